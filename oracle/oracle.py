@@ -1,0 +1,486 @@
+"""ORACLE - test infrastructure only.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg may import this module, and only as the checker (never as the measured or shipped path).
+
+CPU restatement of the reference hot path `LowLevelHumanoidEnv.reset()/step()`:
+
+* env logic (R1-R21) restated line by line from `/root/reference/low_level_env.py` (cited per method),
+  in float64 numpy exactly as the reference computes it (pandas-parsed tables, numpy pairwise means,
+  float32 observation block);
+* `WalkerBase.calc_state` / `Joint.current_relative_position` / `getEulerFromQuaternion`
+  (pybullet_envs + pybullet, third-party, absent here) restated from the published pybullet source;
+* physics through the fp64 C restatement `oracle/physics_oracle.c` (ctypes).
+
+Env-logic parity is PINNED by golden vectors produced by the real reference module
+(`tests/golden/make_golden.py`).  Physics parity vs PyBullet is UNPINNED.
+"""
+import ctypes
+import json
+import math
+import os
+import subprocess
+
+import numpy as np
+from scipy.spatial.transform import Rotation as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libphysoracle.so")
+LINKS = json.load(open(os.path.join(HERE, "humanoid_links.json")))
+ND = 17
+NV = 23
+NSTATE = 47
+DT_ENV = 0.0165
+
+# CustomHumanoidRobot.apply_action gains (humanoid.py:28-37,54-60): motor order -> dof (XML order)
+MOTOR_NAMES = ["abdomen_z", "abdomen_y", "abdomen_x", "right_hip_x", "right_hip_z", "right_hip_y", "right_knee",
+               "left_hip_x", "left_hip_z", "left_hip_y", "left_knee", "right_shoulder_x", "right_shoulder_y",
+               "right_elbow", "left_shoulder_x", "left_shoulder_y", "left_elbow"]
+MOTOR_POWER = [100, 100, 100, 100, 100, 300, 200, 100, 100, 300, 200, 75, 75, 75, 75, 75, 75]
+DOF_NAMES = [d["name"] for d in LINKS["dofs"]]
+MOTOR_DOF = [DOF_NAMES.index(n) for n in MOTOR_NAMES]
+LO = np.array([d["lo"] for d in LINKS["dofs"]])
+HI = np.array([d["hi"] for d in LINKS["dofs"]])
+
+# low_level_env.py:86-137 (dict order matters: it is the summation / observation order)
+JOINT_MAP = [("right_knee", "rightKnee"), ("right_hip_x", "rightHipX"), ("right_hip_y", "rightHipY"),
+             ("right_hip_z", "rightHipZ"), ("left_knee", "leftKnee"), ("left_hip_x", "leftHipX"),
+             ("left_hip_y", "leftHipY"), ("left_hip_z", "leftHipZ"), ("right_shoulder_x", "rightShoulderX"),
+             ("right_shoulder_y", "rightShoulderY"), ("right_elbow", "rightElbow"),
+             ("left_shoulder_x", "leftShoulderX"), ("left_shoulder_y", "leftShoulderY"), ("left_elbow", "leftElbow")]
+JOINT_WEIGHT = {"right_knee": 3, "right_hip_x": 1, "right_hip_y": 3, "right_hip_z": 1, "left_knee": 3,
+                "left_hip_x": 1, "left_hip_y": 3, "left_hip_z": 1, "right_shoulder_x": 0.1,
+                "right_shoulder_y": 0.3, "right_elbow": 0.3, "left_shoulder_x": 0.1, "left_shoulder_y": 0.3,
+                "left_elbow": 0.3}
+JOINT_VEL_WEIGHT = {"right_knee": 1, "right_hip_x": 1, "right_hip_y": 1, "right_hip_z": 1, "left_knee": 1,
+                    "left_hip_x": 1, "left_hip_y": 1, "left_hip_z": 1, "right_shoulder_x": 0.1,
+                    "right_shoulder_y": 0.1, "right_elbow": 0.1, "left_shoulder_x": 0.1, "left_shoulder_y": 0.1,
+                    "left_elbow": 0.1}
+REWARD_WEIGHT = [0.34, 0.1, 0.34, 0.034, 0.15, 0.034, 0.1]   # low_level_env.py:507
+
+
+class OmParams(ctypes.Structure):
+    _fields_ = [("dt", ctypes.c_double), ("nsub", ctypes.c_int), ("gravity", ctypes.c_double),
+                ("iters", ctypes.c_int), ("erp_contact", ctypes.c_double), ("erp_limit", ctypes.c_double),
+                ("mu_ground", ctypes.c_double), ("mu_self", ctypes.c_double), ("contact_thresh", ctypes.c_double),
+                ("lin_damp", ctypes.c_double), ("ang_damp", ctypes.c_double),
+                ("limit_max_impulse", ctypes.c_double), ("max_contacts", ctypes.c_int),
+                ("self_collision", ctypes.c_int), ("joint_damping", ctypes.c_int),
+                ("max_coord_vel", ctypes.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        _lib = ctypes.CDLL(LIB)
+        dp = ctypes.POINTER(ctypes.c_double)
+        _lib.om_step.argtypes = [ctypes.POINTER(OmParams), dp, dp, ctypes.POINTER(ctypes.c_int)]
+        _lib.om_parts.argtypes = [dp, dp]
+        _lib.om_aba.argtypes = [ctypes.POINTER(OmParams), dp, dp, dp]
+        _lib.om_mass_matrix.argtypes = [dp, dp]
+        _lib.om_link_frames.argtypes = [dp, dp, dp]
+        _lib.om_contacts.argtypes = [ctypes.POINTER(OmParams), dp, dp]
+        _lib.om_contacts.restype = ctypes.c_int
+        _lib.om_default_params.argtypes = [ctypes.POINTER(OmParams)]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def default_params():
+    P = OmParams()
+    lib().om_default_params(ctypes.byref(P))
+    return P
+
+
+def phys_step(state, tau_motor, params=None):
+    """One env step of physics (4 substeps) from a 47-state; returns the new state."""
+    P = params or default_params()
+    st = np.array(state, dtype=np.float64).copy()
+    tau = np.ascontiguousarray(tau_motor, dtype=np.float64)
+    nc = ctypes.c_int(0)
+    lib().om_step(ctypes.byref(P), _p(st), _p(tau), ctypes.byref(nc))
+    return st
+
+
+def parts(state):
+    out = np.zeros((33, 3))
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    lib().om_parts(_p(st), _p(out))
+    return out
+
+
+def aba(state, tau, params=None):
+    P = params or default_params()
+    acc = np.zeros(NV)
+    lib().om_aba(ctypes.byref(P), _p(np.ascontiguousarray(state, dtype=np.float64)),
+                 _p(np.ascontiguousarray(tau, dtype=np.float64)), _p(acc))
+    return acc
+
+
+def mass_matrix(state):
+    H = np.zeros((NV, NV))
+    lib().om_mass_matrix(_p(np.ascontiguousarray(state, dtype=np.float64)), _p(H))
+    return H
+
+
+def contacts(state, params=None):
+    P = params or default_params()
+    out = np.zeros((64, 12))
+    n = lib().om_contacts(ctypes.byref(P), _p(np.ascontiguousarray(state, dtype=np.float64)), _p(out))
+    return out[:n]
+
+
+def motor_torques(action):
+    """humanoid.py:54-60: tau[dof] = float(1 * power * 0.41 * clip(a_i)) (action float32 as RLlib passes it)."""
+    a = np.asarray(action)
+    assert np.isfinite(a).all()
+    tau = np.zeros(ND)
+    for i in range(17):
+        tau[MOTOR_DOF[i]] = float(1 * MOTOR_POWER[i] * 0.41 * np.clip(a[i], -1, +1))
+    return tau
+
+
+# ----------------------------------------------------------------------------------------- RNG
+M64 = (1 << 64) - 1
+
+
+def splitmix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def lane_draw(seed, lane, counter, lo, hi):
+    """Counter-based per-lane integer draw in [lo, hi) (replaces the reference's unseeded
+    np.random.default_rng(), low_level_env.py:84; same definition as the product kernel)."""
+    k = splitmix64((seed + lane) & M64)
+    x = splitmix64((k + counter) & M64)
+    return lo + (((x >> 32) * (hi - lo)) >> 32)
+
+
+class LaneRNG:
+    def __init__(self, seed, lane):
+        self.seed, self.lane, self.counter = seed, lane, 0
+
+    def integers(self, lo, hi):
+        v = lane_draw(self.seed, self.lane, self.counter, lo, hi)
+        self.counter += 1
+        return int(v)
+
+
+# ----------------------------------------------------------------------------------------- pybullet restatements
+def euler_from_quaternion(q):
+    """pybullet.getEulerFromQuaternion (x,y,z,w) -> (roll, pitch, yaw)."""
+    x, y, z, w = [float(v) for v in q]
+    squ, sqx, sqy, sqz = w * w, x * x, y * y, z * z
+    roll = math.atan2(2 * (y * z + w * x), squ - sqx - sqy + sqz)
+    sarg = -2 * (x * z - w * y)
+    pitch = -0.5 * 3.141592538 if sarg <= -1.0 else (0.5 * 3.141592538 if sarg >= 1.0 else math.asin(sarg))
+    yaw = math.atan2(2 * (x * y + w * z), squ + sqx - sqy - sqz)
+    return roll, pitch, yaw
+
+
+def relative_joint_state(state):
+    """Joint.current_relative_position for the 17 joints: (2(q-mid)/(hi-lo), 0.1*qd) as float32 pairs."""
+    q, qd = state[13:30], state[30:47]
+    vals = []
+    for i in range(ND):
+        lo, hi = float(LO[i]), float(HI[i])
+        pos_mid = 0.5 * (lo + hi)
+        vals.append((2 * (float(q[i]) - pos_mid) / (hi - lo), float(qd[i]) * 0.1))
+    return np.array(vals, dtype=np.float32).flatten()
+
+
+def calc_state(state, walk_target, initial_z=0.8):
+    """WalkerBase.calc_state (pybullet_envs/robot_locomotors.py), foot_list=[] (humanoid.py:14).
+    Returns (obs42 float32, body_xyz, joint_speeds f32[17], joints_at_limit, rpy)."""
+    j = relative_joint_state(state)
+    joint_speeds = j[1::2]
+    joints_at_limit = np.count_nonzero(np.abs(j[0::2]) > 0.99)
+    pxyz = parts(state).flatten()
+    body_xyz = (pxyz[0::3].mean(), pxyz[1::3].mean(), float(state[2]))
+    r, p, yaw = euler_from_quaternion(state[3:7])
+    z = body_xyz[2]
+    walk_target_theta = np.arctan2(walk_target[1] - body_xyz[1], walk_target[0] - body_xyz[0])
+    angle_to_target = walk_target_theta - yaw
+    rot_speed = np.array([[np.cos(-yaw), -np.sin(-yaw), 0], [np.sin(-yaw), np.cos(-yaw), 0], [0, 0, 1]])
+    vx, vy, vz = np.dot(rot_speed, np.array(state[7:10], dtype=np.float64))
+    more = np.array([z - initial_z, np.sin(angle_to_target), np.cos(angle_to_target), 0.3 * vx, 0.3 * vy,
+                     0.3 * vz, r, p], dtype=np.float32)
+    obs = np.clip(np.concatenate([more] + [j] + [np.zeros(0, dtype=np.float32)]), -5, +5)
+    return obs, body_xyz, joint_speeds, joints_at_limit, (r, p, yaw)
+
+
+def get_joint_pos(clip, row, joint):
+    """low_level_env.py:23-27 getJointPos on the end-point table."""
+    return np.array([clip.ep[row, clip.ecol(joint + "_Xposition")], clip.ep[row, clip.ecol(joint + "_Yposition")],
+                     clip.ep[row, clip.ecol(joint + "_Zposition")]])
+
+
+# ----------------------------------------------------------------------------------------- env
+class OracleLowLevelEnv:
+    """Single-lane restatement of LowLevelHumanoidEnv (low_level_env.py:36-526)."""
+
+    def __init__(self, clip, seed=0, lane=0, params=None, rng=None):
+        self.clip = clip
+        self.params = params
+        self.cur_timestep = 0
+        self.max_timestep = 3000                                    # :73
+        self.frame = 0
+        self.max_frame = clip.pos.shape[0] - 1                      # :80-82
+        self.rng = rng if rng is not None else LaneRNG(seed, lane)  # :84 (explicit, counter based)
+        self.joint_weight_sum = sum(JOINT_WEIGHT.values())          # :119
+        self.joint_vel_weight_sum = sum(JOINT_VEL_WEIGHT.values())  # :137
+        self.target = np.array([1, 0, 0])                           # :154
+        self.targetLen = 5
+        self.highLevelDegTarget = 0
+        self.predefinedTarget = np.array([[]])
+        self.predefinedTargetIndex = 0
+        self.usePredefinedTarget = False
+        self.skipFrame = 2                                          # :162
+        self.starting_ep_pos = np.array([0, 0, 0])
+        self.starting_robot_pos = np.array([0, 0, 0])
+        self.robot_pos = np.array([0, 0, 0])
+        self.walk_target = (10.0, 0.0)
+        self.state = np.zeros(NSTATE)
+        self.state[6] = 1.0
+        self.cur_obs = np.zeros(42, dtype=np.float32)
+        self.joint_speeds = np.zeros(17, dtype=np.float32)
+        self.joints_at_limit = 0
+        self.rpy = (0.0, 0.0, 0.0)
+        self.initReward()
+
+    def initReward(self):                                           # :174-197
+        self.deltaJoints = 0
+        self.deltaVelJoints = 0
+        self.deltaEndPoints = 0
+        self.baseReward = 0
+        self.lowTargetScore = 0
+        self.last_lowTargetScore = 0
+        self.aliveReward = 0
+        self.electricityScore = 0
+        self.jointLimitScore = 0
+        self.bodyPostureScore = 0
+        self.bodySpeedScore = 0
+        self.highTargetScore = 0
+        self.driftScore = 0
+        self.cumulative_driftScore = 0
+        self.delta_deltaJoints = 0
+        self.delta_deltaVelJoints = 0
+        self.delta_deltaEndPoints = 0
+        self.delta_lowTargetScore = 0
+        self.delta_bodyPostureScore = 0
+        self.delta_highTargetScore = 0
+
+    # -- physics-facing helpers (stand in for flat_env / robot) ----------------------------------------
+    def _calc_state(self):
+        obs, body_xyz, js, jal, rpy = calc_state(self.state, self.walk_target)
+        self.body_xyz, self.joint_speeds, self.joints_at_limit, self.rpy = body_xyz, js, jal, rpy
+        return obs
+
+    def setJointsOrientation(self, idx):                            # :205-216
+        c = self.clip
+        for name in ("abdomen_x", "abdomen_y", "abdomen_z"):
+            d = DOF_NAMES.index(name)
+            self.state[13 + d] = 0
+            self.state[30 + d] = 0
+        for joint, col in JOINT_MAP:
+            d = DOF_NAMES.index(joint)
+            self.state[13 + d] = c.pos[idx, c.jcol(col)]
+            self.state[30 + d] = c.vel[idx, c.jcol(col)]
+
+    def incFrame(self, inc):                                        # :218-222
+        self.frame = (self.frame + inc) % (self.max_frame - 1)
+        if self.frame == 0:
+            self.starting_ep_pos = self.robot_pos.copy()
+
+    def reset(self, resetYaw=0):                                    # :224-232
+        return self.resetFromFrame(startFrame=self.rng.integers(0, self.max_frame - 5), resetYaw=resetYaw,
+                                   startFromRef=True, initVel=True)
+
+    def setWalkTarget(self, x, y):                                  # :234-238
+        self.walk_target = (x, y)
+
+    def getRandomVec(self, vecLen, z, initYaw=0):                   # :240-245
+        randomRad = initYaw + np.deg2rad(self.rng.integers(-180, 180))
+        return np.array([np.cos(randomRad) * vecLen, np.sin(randomRad) * vecLen, z])
+
+    def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):  # :247-305
+        # flat_env.reset(): restoreState -> zero velocities; robot_specific_reset re-randomises joints
+        # (all 17 are overwritten below when startFromRef)
+        self.state[:] = 0
+        self.state[6] = 1.0
+        self.cur_timestep = 0
+        if self.usePredefinedTarget:
+            self.predefinedTargetIndex = 0
+            self.target = self.predefinedTarget[self.predefinedTargetIndex].copy()
+        else:
+            self.target = self.getRandomVec(self.targetLen, 0)
+        if startFromRef:
+            self.frame = startFrame
+            self.setJointsOrientation(self.frame)
+        robotPos = np.array([0, 0, 1.17])
+        self.robot_pos = np.array([robotPos[0], robotPos[1], 0])
+        self.last_robotPos = self.robot_pos.copy()
+        self.starting_robot_pos = self.robot_pos.copy()
+        self.state[0:3] = robotPos
+        degToTarget = np.rad2deg(np.arctan2(self.target[1], self.target[0]))
+        self.setWalkTarget(np.cos(degToTarget) * 1000, np.sin(degToTarget) * 1000)
+        robotRot = R.from_euler("z", degToTarget + resetYaw, degrees=True)
+        self.state[3:7] = robotRot.as_quat()
+        self.highLevelDegTarget = np.deg2rad(degToTarget)
+        endPointRef = self.frame
+        endPointRefNext = (self.frame + self.skipFrame) % self.max_frame
+        pxyz = parts(self.state)
+        rightFootPosActual = pxyz[[p["name"] for p in LINKS["parts"]].index("right_foot")].copy()
+        rightFootPosActual[2] = 0
+        rotDeg = R.from_euler("z", degToTarget, degrees=True)
+        rightFootPosRef = rotDeg.apply(get_joint_pos(self.clip, endPointRef, "RightFoot"))
+        rightFootPosRef[2] = 0
+        self.starting_ep_pos = rightFootPosActual - rightFootPosRef
+        if startFromRef and initVel:
+            rightLegPosRef = rotDeg.apply(get_joint_pos(self.clip, endPointRef, "RightLeg"))
+            rightLegPosRefNext = rotDeg.apply(get_joint_pos(self.clip, endPointRefNext, "RightLeg"))
+            startingVelocity = ((rightLegPosRefNext - rightLegPosRef) / 0.0165) / 1.2
+            self.state[7:10] = startingVelocity
+            self.state[10:13] = 0
+        self.initReward()
+        self.frame_update_cnt = 0
+        self.incFrame(self.skipFrame)
+        self.cur_obs = self._calc_state()
+        return self.getLowLevelObs()
+
+    def getLowLevelObs(self):                                       # :307-320
+        c = self.clip
+        jt = []
+        for _, col in JOINT_MAP:
+            jt.append(c.rel[self.frame, c.jcol(col)])
+            jt.append(c.vel[self.frame, c.jcol(col)])
+        return np.hstack((self.cur_obs, np.array(jt)))
+
+    def calcJointScore(self, useExp=False):                         # :325-341
+        deltaJoints = 0
+        c = self.clip
+        for jm, col in JOINT_MAP:
+            deltaJoints += np.abs(self.state[13 + DOF_NAMES.index(jm)] - c.pos[self.frame, c.jcol(col)]) * JOINT_WEIGHT[jm]
+        score = -deltaJoints / self.joint_weight_sum
+        if useExp:
+            score = np.exp(4 * score)
+        return score
+
+    def calcJointVelScore(self, useExp=False):                      # :343-359
+        deltaVel = 0
+        c = self.clip
+        for jm, col in JOINT_MAP:
+            deltaVel += np.abs(self.state[30 + DOF_NAMES.index(jm)] - c.vel[self.frame, c.jcol(col)]) * JOINT_VEL_WEIGHT[jm]
+        score = -deltaVel / self.joint_vel_weight_sum
+        if useExp:
+            score = np.exp(score / 2)
+        return score
+
+    def calcEndPointScore(self, useExp=False):                      # :361-382 (not on the reward path)
+        endpoint_map = [("link0_11", "RightLeg", 1), ("right_foot", "RightFoot", 3), ("link0_18", "LeftLeg", 1),
+                        ("left_foot", "LeftFoot", 3)]
+        names = [p["name"] for p in LINKS["parts"]]
+        pxyz = parts(self.state)
+        r = R.from_euler("z", self.highLevelDegTarget)
+        d = 0
+        for part, ref, w in endpoint_map:
+            v1 = pxyz[names.index(part)]
+            v2 = self.starting_ep_pos + r.apply(get_joint_pos(self.clip, self.frame, ref))
+            d += np.linalg.norm(v2 - v1) * w
+        score = -d / 8
+        return np.exp(3 * score) if useExp else score
+
+    def calcAliveReward(self):                                      # :384-387
+        z = self.cur_obs[0] + 0.8
+        return +2 if z > 0.75 else -1
+
+    def calcElectricityCost(self, action):                          # :389-394
+        runningCost = -1.0 * float(np.abs(action * self.joint_speeds).mean())
+        stallCost = -0.1 * float(np.square(action).mean())
+        return runningCost + stallCost
+
+    def calcJointLimitCost(self):                                   # :396-397
+        return -0.1 * self.joints_at_limit
+
+    def calcLowLevelTargetScore(self):                              # :399-403
+        return -np.linalg.norm(self.target - self.robot_pos)
+
+    def calcBodyPostureScore(self, useExp=False):                   # :405-410
+        roll, pitch, yaw = self.rpy_now()
+        score = -(np.abs(yaw - self.highLevelDegTarget) + np.abs(roll) + np.abs(pitch))
+        return np.exp(score) if useExp else score
+
+    def rpy_now(self):
+        return euler_from_quaternion(self.state[3:7])
+
+    def checkTarget(self):                                          # :412-434
+        distToTarget = np.linalg.norm(self.robot_pos - self.target)
+        if distToTarget <= 0.5:
+            _, _, yaw = self.rpy_now()
+            randomTarget = self.getRandomVec(self.targetLen, 0, initYaw=yaw)
+            newTarget = self.robot_pos + randomTarget
+            if self.usePredefinedTarget:
+                self.predefinedTargetIndex = (self.predefinedTargetIndex + 1) % len(self.predefinedTarget)
+                newTarget = self.predefinedTarget[self.predefinedTargetIndex]
+            self.starting_robot_pos = self.target.copy()
+            self.target = newTarget
+            self.lowTargetScore = -np.linalg.norm(self.target - self.starting_robot_pos)
+        vRobotTarget = self.target - self.robot_pos
+        self.highLevelDegTarget = np.arctan2(vRobotTarget[1], vRobotTarget[0])
+        self.setWalkTarget(self.robot_pos[0] + np.cos(self.highLevelDegTarget) * 10,
+                           self.robot_pos[1] + np.sin(self.highLevelDegTarget) * 10)
+
+    def updateReward(self, action):                                 # :441-465
+        jointScore = self.calcJointScore(useExp=True)
+        jointVelScore = self.calcJointVelScore(useExp=True)
+        lowTargetScore = self.calcLowLevelTargetScore()
+        bodyPostureScore = self.calcBodyPostureScore(useExp=True)
+        self.delta_deltaJoints = (jointScore - self.deltaJoints) / 0.0165
+        self.delta_deltaVelJoints = (jointVelScore - self.deltaVelJoints) / 0.0165 * 0.1
+        self.delta_lowTargetScore = (lowTargetScore - self.lowTargetScore) / 0.0165 * 0.1
+        self.delta_bodyPostureScore = (bodyPostureScore - self.bodyPostureScore) / 0.0165 * 0.1
+        self.deltaJoints = jointScore
+        self.deltaVelJoints = jointVelScore
+        self.lowTargetScore = lowTargetScore
+        self.electricityScore = self.calcElectricityCost(action)
+        self.jointLimitScore = self.calcJointLimitCost()
+        self.aliveReward = self.calcAliveReward()
+        self.bodyPostureScore = bodyPostureScore
+
+    def checkIfDone(self, debug=False):                             # :467-473
+        isAlive = self.aliveReward > 0
+        isNearTarget = np.linalg.norm(self.target - self.robot_pos) <= \
+            np.linalg.norm(self.target - self.starting_robot_pos) + 3
+        return (not isAlive) if debug else (not (isAlive and isNearTarget))
+
+    def step(self, action, debug=False, physics=True):              # :475-526
+        action = np.asarray(action, dtype=np.float32)
+        if physics:
+            self.state = phys_step(self.state, motor_torques(action), self.params)
+        self.cur_obs = self._calc_state()
+        self.robot_pos[0] = self.body_xyz[0]
+        self.robot_pos[1] = self.body_xyz[1]
+        self.robot_pos[2] = 0
+        self.updateReward(action=action)
+        reward = [self.deltaJoints, self.deltaVelJoints, self.delta_lowTargetScore, self.electricityScore,
+                  self.jointLimitScore, self.aliveReward, self.bodyPostureScore]
+        totalReward = 0
+        for r, w in zip(reward, REWARD_WEIGHT):
+            totalReward += r * w
+        self.incFrame(self.skipFrame)
+        self.checkTarget()
+        obs = self.getLowLevelObs()
+        done = self.checkIfDone(debug=debug)
+        self.cur_timestep += 1
+        if self.cur_timestep >= self.max_timestep:
+            done = True
+        return obs, totalReward, done, {}

@@ -1,0 +1,706 @@
+/* ORACLE - test infrastructure only (imported by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the CHECKER; never linked into or called by the product path).
+ *
+ * CPU fp64 restatement of the rigid-multibody step that LowLevelHumanoidEnv.step() drives through
+ * pybullet (reference: low_level_env.py:478-481 -> humanoid.py:54-60 apply_action -> pybullet
+ * stepSimulation).  The physics lives in the third-party Bullet library (btMultiBody /
+ * btMultiBodyConstraintSolver inside the `pybullet` wheel, version unknown, NOT present in
+ * /root/reference or this image), so this file restates Bullet's published algorithm:
+ *
+ *   per env step: motor torques tau = 0.41*power*clip(a) (held over the substeps, as pybullet keeps
+ *   TORQUE_CONTROL forces until stepSimulation returns); MJCF joint damping is integrated implicitly
+ *   per substep (Bullet ignores MJCF armature, and explicit damping is unstable for this model)
+ *   4 substeps of dt = 0.0165/4 (pybullet_envs World: fixedTimeStep 0.0165, numSubSteps 4), each:
+ *     1. collision detection at the current pose (geom vs plane z=0, geom vs geom self-collision
+ *        excluding ancestors; contact breaking threshold 0.02)
+ *     2. Featherstone articulated-body algorithm in LOCAL link frames over pybullet's 32-link layout
+ *        (zero-mass dummy links for every hinge, fixed links for bodies), gravity 9.8, Bullet's
+ *        default link damping (linear/angular 0.04, velocity + velocity^2 terms), gyroscopic terms;
+ *        velocities <- velocities + dt * accelerations (btMultiBody semi-implicit Euler)
+ *     3. constraint rows built on those velocities, btMultiBodyConstraintSolver order:
+ *        joint-limit rows (violated limits only, erp 0.2, impulse <= 100), contact normal rows
+ *        (erp 0.9 = setDefaultContactERP, speculative -d/dt when separated), two friction rows per
+ *        contact (mu = 2.0*0.8 ground / 2.0*2.0 self, box bounds +-mu*lambda_n); PGS, 5 iterations;
+ *        the constraint responses use the joint-space mass matrix H (built from link Jacobians) and
+ *        its Cholesky factor - an independent route to the same M^-1 J^T the product kernel gets
+ *        from its ABA factorisation
+ *     4. positions <- positions + dt * velocities (base orientation by Bullet's exponential map)
+ *
+ * PARITY vs PyBullet: UNPINNED (pybullet absent; no reference test pins physics). See DESIGN.md.
+ *
+ * State vector (47 doubles, shared with the product C-ABI): base pos[3] (COM, world), base quat[4]
+ * (x,y,z,w), base lin vel[3] (COM, world), base ang vel[3] (world), q[17], qd[17] (XML dof order).
+ */
+#include <math.h>
+#include <string.h>
+
+#include "humanoid_links_gen.h"
+
+#define NV (6 + OM_ND)
+#define MAXC 64
+#define MAXROW (3 * MAXC + 2 * OM_ND)
+
+typedef struct {
+    double dt;              /* substep */
+    int nsub;               /* substeps per env step */
+    double gravity;
+    int iters;              /* PGS iterations */
+    double erp_contact, erp_limit, mu_ground, mu_self, contact_thresh;
+    double lin_damp, ang_damp, limit_max_impulse;
+    int max_contacts;
+    int self_collision;
+    int joint_damping;      /* 0: ignore MJCF joint damping, 1: implicit per substep (default) */
+    double max_coord_vel;   /* btMultiBody::m_maxCoordinateVelocity clamp in applyDeltaVeeMultiDof */
+} om_params;
+
+/* ------------------------------------------------------------------------- small linear algebra */
+static void mat3_mul(const double* A, const double* B, double* C) {
+    double T[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    memcpy(C, T, sizeof T);
+}
+static void mat3_vec(const double* A, const double* x, double* y) {
+    double t[3];
+    for (int i = 0; i < 3; i++) t[i] = A[3 * i] * x[0] + A[3 * i + 1] * x[1] + A[3 * i + 2] * x[2];
+    memcpy(y, t, sizeof t);
+}
+static void mat3T_vec(const double* A, const double* x, double* y) {
+    double t[3];
+    for (int i = 0; i < 3; i++) t[i] = A[i] * x[0] + A[3 + i] * x[1] + A[6 + i] * x[2];
+    memcpy(y, t, sizeof t);
+}
+static void cross(const double* a, const double* b, double* c) {
+    double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    memcpy(c, t, sizeof t);
+}
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double norm3(const double* a) { return sqrt(dot3(a, a)); }
+
+static void axis_angle(const double* u, double q, double* R) {
+    double c = cos(q), s = sin(q), C = 1 - c;
+    double x = u[0], y = u[1], z = u[2];
+    R[0] = c + x * x * C;     R[1] = x * y * C - z * s; R[2] = x * z * C + y * s;
+    R[3] = y * x * C + z * s; R[4] = c + y * y * C;     R[5] = y * z * C - x * s;
+    R[6] = z * x * C - y * s; R[7] = z * y * C + x * s; R[8] = c + z * z * C;
+}
+static void quat_to_mat(const double* q, double* R) { /* q = x,y,z,w */
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
+    R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+    R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
+}
+
+/* --------------------------------------------------------------------------- kinematics */
+typedef struct {
+    double R[OM_NL][9];   /* link frame -> world */
+    double x[OM_NL][3];   /* link origin, world */
+    double E[OM_NL][9];   /* parent coords -> link coords (rotation part of X) */
+} om_kin;
+
+static void fk(const double* st, om_kin* K) {
+    quat_to_mat(st + 3, K->R[0]);
+    memcpy(K->x[0], st, 3 * sizeof(double));
+    for (int l = 1; l < OM_NL; l++) {
+        int p = om_parent[l];
+        double Rl[9];
+        if (om_type[l] == 1) {
+            double Ra[9];
+            axis_angle(om_axis + 3 * l, st[13 + om_dof[l]], Ra);
+            mat3_mul(om_Rfix + 9 * l, Ra, Rl);       /* parent <- link */
+        } else {
+            memcpy(Rl, om_Rfix + 9 * l, sizeof Rl);
+        }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) K->E[l][3 * i + j] = Rl[3 * j + i];   /* transpose: link <- parent */
+        mat3_mul(K->R[p], Rl, K->R[l]);
+        double d[3];
+        mat3_vec(K->R[p], om_t + 3 * l, d);
+        for (int i = 0; i < 3; i++) K->x[l][i] = K->x[p][i] + d[i];
+    }
+}
+
+void om_parts(const double* st, double* out /* [OM_NPART][3] */) {
+    om_kin K;
+    fk(st, &K);
+    for (int k = 0; k < OM_NPART; k++) {
+        int l = om_part_link[k];
+        if (l < 0) { out[3 * k] = out[3 * k + 1] = out[3 * k + 2] = 0.0; continue; }
+        double d[3];
+        mat3_vec(K.R[l], om_part_p + 3 * k, d);
+        for (int i = 0; i < 3; i++) out[3 * k + i] = K.x[l][i] + d[i];
+    }
+}
+
+/* world position of a point given in link coords */
+static void link_point(const om_kin* K, int l, const double* p, double* w) {
+    double d[3];
+    mat3_vec(K->R[l], p, d);
+    for (int i = 0; i < 3; i++) w[i] = K->x[l][i] + d[i];
+}
+
+/* --------------------------------------------------------------------------- Jacobians / mass matrix */
+/* Generalised velocity nu = [w(3) world, v(3) base COM world, qd(ND)]. */
+/* point Jacobian (3 x NV, row major) of a world point p rigidly attached to link l */
+static void point_jacobian(const om_kin* K, int l, const double* p, double* J) {
+    memset(J, 0, 3 * NV * sizeof(double));
+    double d[3] = {p[0] - K->x[0][0], p[1] - K->x[0][1], p[2] - K->x[0][2]};
+    /* w x d = -d x w  -> columns of -[d]x */
+    J[0 * NV + 0] = 0;     J[0 * NV + 1] = d[2];  J[0 * NV + 2] = -d[1];
+    J[1 * NV + 0] = -d[2]; J[1 * NV + 1] = 0;     J[1 * NV + 2] = d[0];
+    J[2 * NV + 0] = d[1];  J[2 * NV + 1] = -d[0]; J[2 * NV + 2] = 0;
+    J[0 * NV + 3] = 1; J[1 * NV + 4] = 1; J[2 * NV + 5] = 1;
+    for (int k = l; k > 0; k = om_parent[k]) {
+        if (om_type[k] != 1) continue;
+        double u[3], r[3], c[3];
+        mat3_vec(K->R[k], om_axis + 3 * k, u);
+        for (int i = 0; i < 3; i++) r[i] = p[i] - K->x[k][i];
+        cross(u, r, c);
+        int col = 6 + om_dof[k];
+        for (int i = 0; i < 3; i++) J[i * NV + col] = c[i];
+    }
+}
+static void ang_jacobian(const om_kin* K, int l, double* J) {
+    memset(J, 0, 3 * NV * sizeof(double));
+    J[0 * NV + 0] = 1; J[1 * NV + 1] = 1; J[2 * NV + 2] = 1;
+    for (int k = l; k > 0; k = om_parent[k]) {
+        if (om_type[k] != 1) continue;
+        double u[3];
+        mat3_vec(K->R[k], om_axis + 3 * k, u);
+        int col = 6 + om_dof[k];
+        for (int i = 0; i < 3; i++) J[i * NV + col] = u[i];
+    }
+}
+
+static void mass_matrix(const om_kin* K, double* H) {
+    memset(H, 0, NV * NV * sizeof(double));
+    double Jp[3 * NV], Jw[3 * NV];
+    for (int l = 0; l < OM_NL; l++) {
+        double m = om_mass[l];
+        if (m <= 0) continue;
+        double c[3], Iw[9], T[9], RT[9];
+        link_point(K, l, om_com + 3 * l, c);
+        point_jacobian(K, l, c, Jp);
+        ang_jacobian(K, l, Jw);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) RT[3 * i + j] = K->R[l][3 * j + i];
+        mat3_mul(K->R[l], om_inertia + 9 * l, T);
+        mat3_mul(T, RT, Iw);
+        for (int a = 0; a < NV; a++)
+            for (int b = 0; b < NV; b++) {
+                double s = 0;
+                for (int i = 0; i < 3; i++) s += m * Jp[i * NV + a] * Jp[i * NV + b];
+                for (int i = 0; i < 3; i++)
+                    for (int j = 0; j < 3; j++) s += Jw[i * NV + a] * Iw[3 * i + j] * Jw[j * NV + b];
+                H[a * NV + b] += s;
+            }
+    }
+}
+
+static int cholesky(double* A, int n) { /* in place, lower */
+    for (int j = 0; j < n; j++) {
+        double s = A[j * n + j];
+        for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+        if (s <= 0) return -1;
+        A[j * n + j] = sqrt(s);
+        for (int i = j + 1; i < n; i++) {
+            double t = A[i * n + j];
+            for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = t / A[j * n + j];
+        }
+    }
+    return 0;
+}
+static void chol_solve(const double* L, int n, double* b) {
+    for (int i = 0; i < n; i++) {
+        double s = b[i];
+        for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s = b[i];
+        for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+}
+
+/* --------------------------------------------------------------------------- spatial algebra (local frames) */
+/* motion/force 6-vectors are [angular; linear]. */
+static void crm(const double* v, const double* m, double* r) { /* v x m */
+    double a[3], b[3], c[3];
+    cross(v, m, a);
+    cross(v, m + 3, b);
+    cross(v + 3, m, c);
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+    r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+static void crf(const double* v, const double* f, double* r) { /* v x* f */
+    double a[3], b[3], c[3];
+    cross(v, f, a);
+    cross(v + 3, f + 3, b);
+    cross(v, f + 3, c);
+    r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+    r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+/* spatial inertia at link origin, link coords, 6x6 row major */
+static void spatial_inertia(int l, double* I6) {
+    double m = om_mass[l];
+    const double* c = om_com + 3 * l;
+    const double* Ic = om_inertia + 9 * l;
+    double cc = dot3(c, c);
+    double cx[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+    memset(I6, 0, 36 * sizeof(double));
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            I6[6 * i + j] = Ic[3 * i + j] + m * ((i == j ? cc : 0) - c[i] * c[j]);
+            I6[6 * i + 3 + j] = m * cx[3 * i + j];
+            I6[6 * (3 + i) + j] = m * cx[3 * j + i];   /* (m c x)^T */
+            I6[6 * (3 + i) + 3 + j] = (i == j) ? m : 0;
+        }
+}
+static void mat6_vec(const double* A, const double* x, double* y) {
+    double t[6];
+    for (int i = 0; i < 6; i++) {
+        double s = 0;
+        for (int j = 0; j < 6; j++) s += A[6 * i + j] * x[j];
+        t[i] = s;
+    }
+    memcpy(y, t, sizeof t);
+}
+/* X (parent->link) as a full 6x6: [[E,0],[-E rx, E]] */
+static void build_X(const double* E, const double* r, double* X) {
+    double rx[9] = {0, -r[2], r[1], r[2], 0, -r[0], -r[1], r[0], 0};
+    double Erx[9];
+    mat3_mul(E, rx, Erx);
+    memset(X, 0, 36 * sizeof(double));
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            X[6 * i + j] = E[3 * i + j];
+            X[6 * (3 + i) + 3 + j] = E[3 * i + j];
+            X[6 * (3 + i) + j] = -Erx[3 * i + j];
+        }
+}
+
+/* ABA: generalised accelerations (nu-dot, base classical accel in world) for state st, joint torques tau.
+ * Returns acc[NV] = [w_dot world, v_com_dot world, qdd]. */
+static void aba(const om_params* P, const double* st, const om_kin* K, const double* tau, double* acc) {
+    double X[OM_NL][36], v[OM_NL][6], c[OM_NL][6], IA[OM_NL][36], pA[OM_NL][6];
+    double U[OM_NL][6], D[OM_NL], u[OM_NL], a[OM_NL][6];
+    const double g[3] = {0, 0, -P->gravity};
+    /* base velocity in base coords */
+    double wl[3], vl[3];
+    mat3T_vec(K->R[0], st + 10, wl);
+    mat3T_vec(K->R[0], st + 7, vl);
+    for (int l = 0; l < OM_NL; l++) {
+        if (l == 0) {
+            v[0][0] = wl[0]; v[0][1] = wl[1]; v[0][2] = wl[2];
+            v[0][3] = vl[0]; v[0][4] = vl[1]; v[0][5] = vl[2];
+            memset(c[0], 0, sizeof c[0]);
+        } else {
+            int p = om_parent[l];
+            build_X(K->E[l], om_t + 3 * l, X[l]);
+            mat6_vec(X[l], v[p], v[l]);
+            memset(c[l], 0, sizeof c[l]);
+            if (om_type[l] == 1) {
+                double qd = st[30 + om_dof[l]];
+                double Sq[6] = {om_axis[3 * l] * qd, om_axis[3 * l + 1] * qd, om_axis[3 * l + 2] * qd, 0, 0, 0};
+                for (int i = 0; i < 6; i++) v[l][i] += Sq[i];
+                crm(v[l], Sq, c[l]);
+            }
+        }
+        spatial_inertia(l, IA[l]);
+        double Iv[6];
+        mat6_vec(IA[l], v[l], Iv);
+        crf(v[l], Iv, pA[l]);
+        /* external: gravity + Bullet link damping, applied at the COM */
+        double m = om_mass[l];
+        if (m > 0) {
+            const double* cm = om_com + 3 * l;
+            double gl[3], vcom[3], wxc[3], F[3], n[3], Iw[3];
+            mat3T_vec(K->R[l], g, gl);
+            cross(v[l], cm, wxc);
+            for (int i = 0; i < 3; i++) vcom[i] = v[l][3 + i] + wxc[i];
+            double kv = P->lin_damp + P->lin_damp * norm3(vcom);
+            double kw = P->ang_damp + P->ang_damp * norm3(v[l]);
+            mat3_vec(om_inertia + 9 * l, v[l], Iw);
+            for (int i = 0; i < 3; i++) {
+                F[i] = m * gl[i] - m * vcom[i] * kv;
+                n[i] = -Iw[i] * kw;
+            }
+            double cxF[3];
+            cross(cm, F, cxF);
+            for (int i = 0; i < 3; i++) {
+                pA[l][i] -= n[i] + cxF[i];
+                pA[l][3 + i] -= F[i];
+            }
+        }
+    }
+    for (int l = OM_NL - 1; l >= 1; l--) {
+        int p = om_parent[l];
+        double Ia[36], pa[6];
+        memcpy(Ia, IA[l], sizeof Ia);
+        memcpy(pa, pA[l], sizeof pa);
+        if (om_type[l] == 1) {
+            const double* ax = om_axis + 3 * l;
+            double S[6] = {ax[0], ax[1], ax[2], 0, 0, 0};
+            mat6_vec(IA[l], S, U[l]);
+            D[l] = 0;
+            for (int i = 0; i < 6; i++) D[l] += S[i] * U[l][i];
+            double Sp = 0;
+            for (int i = 0; i < 6; i++) Sp += S[i] * pA[l][i];
+            u[l] = tau[om_dof[l]] - Sp;
+            if (P->joint_damping) {   /* implicit Euler on -d*qd: (D + dt d) qdd = u - d qd */
+                double dmp = om_jdamp[om_dof[l]];
+                D[l] += P->dt * dmp;
+                u[l] -= dmp * st[30 + om_dof[l]];
+            }
+            for (int i = 0; i < 6; i++)
+                for (int j = 0; j < 6; j++) Ia[6 * i + j] -= U[l][i] * U[l][j] / D[l];
+            double Iac[6];
+            mat6_vec(Ia, c[l], Iac);
+            for (int i = 0; i < 6; i++) pa[i] = pA[l][i] + Iac[i] + U[l][i] * u[l] / D[l];
+        } else {
+            double Iac[6];
+            mat6_vec(Ia, c[l], Iac);
+            for (int i = 0; i < 6; i++) pa[i] += Iac[i];
+        }
+        /* IA_p += X^T Ia X ; pA_p += X^T pa */
+        double T[36];
+        for (int i = 0; i < 6; i++)
+            for (int j = 0; j < 6; j++) {
+                double s = 0;
+                for (int k = 0; k < 6; k++) s += Ia[6 * i + k] * X[l][6 * k + j];
+                T[6 * i + j] = s;
+            }
+        for (int i = 0; i < 6; i++)
+            for (int j = 0; j < 6; j++) {
+                double s = 0;
+                for (int k = 0; k < 6; k++) s += X[l][6 * k + i] * T[6 * k + j];
+                IA[p][6 * i + j] += s;
+            }
+        for (int i = 0; i < 6; i++) {
+            double s = 0;
+            for (int k = 0; k < 6; k++) s += X[l][6 * k + i] * pa[k];
+            pA[p][i] += s;
+        }
+    }
+    /* base: a0 = -IA0^{-1} pA0 */
+    {
+        double L[36], b[6];
+        memcpy(L, IA[0], sizeof L);
+        cholesky(L, 6);
+        for (int i = 0; i < 6; i++) b[i] = -pA[0][i];
+        chol_solve(L, 6, b);
+        memcpy(a[0], b, sizeof b);
+    }
+    for (int l = 1; l < OM_NL; l++) {
+        int p = om_parent[l];
+        double ap[6];
+        mat6_vec(X[l], a[p], ap);
+        for (int i = 0; i < 6; i++) a[l][i] = ap[i] + c[l][i];
+        if (om_type[l] == 1) {
+            double Ua = 0;
+            for (int i = 0; i < 6; i++) Ua += U[l][i] * a[l][i];
+            double qdd = (u[l] - Ua) / D[l];
+            acc[6 + om_dof[l]] = qdd;
+            const double* ax = om_axis + 3 * l;
+            a[l][0] += ax[0] * qdd; a[l][1] += ax[1] * qdd; a[l][2] += ax[2] * qdd;
+        }
+    }
+    /* base: spatial -> classical, base coords -> world */
+    double wd[3], lin[3], wxv[3];
+    cross(wl, vl, wxv);
+    for (int i = 0; i < 3; i++) lin[i] = a[0][3 + i] + wxv[i];
+    mat3_vec(K->R[0], a[0], wd);
+    double ld[3];
+    mat3_vec(K->R[0], lin, ld);
+    for (int i = 0; i < 3; i++) { acc[i] = wd[i]; acc[3 + i] = ld[i]; }
+}
+
+/* --------------------------------------------------------------------------- collision */
+typedef struct {
+    int la, lb;         /* links; lb = -1 for ground */
+    double pa[3], pb[3]; /* contact points on A and B (world) */
+    double n[3];        /* normal, from B to A */
+    double d;           /* signed distance (<0 penetration) */
+    double mu;
+} om_contact;
+
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* closest points between segments p1q1 and p2q2 (Ericson, Real-Time Collision Detection 5.1.9) */
+static void seg_seg(const double* p1, const double* q1, const double* p2, const double* q2, double* c1, double* c2) {
+    double d1[3], d2[3], r[3];
+    for (int i = 0; i < 3; i++) { d1[i] = q1[i] - p1[i]; d2[i] = q2[i] - p2[i]; r[i] = p1[i] - p2[i]; }
+    double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    double s, t;
+    const double EPS = 1e-12;
+    if (a <= EPS && e <= EPS) { s = t = 0; }
+    else if (a <= EPS) { s = 0; t = clampd(f / e, 0, 1); }
+    else {
+        double c = dot3(d1, r);
+        if (e <= EPS) { t = 0; s = clampd(-c / a, 0, 1); }
+        else {
+            double b = dot3(d1, d2), den = a * e - b * b;
+            s = (den > EPS) ? clampd((b * f - c * e) / den, 0, 1) : 0;
+            t = (b * s + f) / e;
+            if (t < 0) { t = 0; s = clampd(-c / a, 0, 1); }
+            else if (t > 1) { t = 1; s = clampd((b - c) / a, 0, 1); }
+        }
+    }
+    for (int i = 0; i < 3; i++) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
+}
+
+static int collide(const om_params* P, const om_kin* K, om_contact* C) {
+    int nc = 0;
+    double gp1[OM_NG][3], gp2[OM_NG][3];
+    for (int g = 0; g < OM_NG; g++) {
+        link_point(K, om_glink[g], om_gp1 + 3 * g, gp1[g]);
+        link_point(K, om_glink[g], om_gp2 + 3 * g, gp2[g]);
+    }
+    for (int g = 0; g < OM_NG; g++) {
+        int ne = om_gtype[g] == 0 ? 1 : 2;
+        for (int e = 0; e < ne; e++) {
+            const double* p = e == 0 ? gp1[g] : gp2[g];
+            double d = p[2] - om_gr[g];
+            if (d < P->contact_thresh && nc < P->max_contacts) {
+                om_contact* c = &C[nc++];
+                c->la = om_glink[g]; c->lb = -1;
+                c->pa[0] = p[0]; c->pa[1] = p[1]; c->pa[2] = p[2] - om_gr[g];
+                c->pb[0] = p[0]; c->pb[1] = p[1]; c->pb[2] = 0;
+                c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
+                c->d = d; c->mu = P->mu_ground;
+            }
+        }
+    }
+    if (P->self_collision) {
+        for (int k = 0; k < OM_NPAIR; k++) {
+            int ga = om_pair_a[k], gb = om_pair_b[k];
+            double ca[3], cb[3], dv[3];
+            seg_seg(gp1[ga], gp2[ga], gp1[gb], gp2[gb], ca, cb);
+            for (int i = 0; i < 3; i++) dv[i] = ca[i] - cb[i];
+            double dist = norm3(dv);
+            double d = dist - om_gr[ga] - om_gr[gb];
+            if (d < P->contact_thresh && dist > 1e-9 && nc < P->max_contacts) {
+                om_contact* c = &C[nc++];
+                c->la = om_glink[ga]; c->lb = om_glink[gb];
+                for (int i = 0; i < 3; i++) {
+                    c->n[i] = dv[i] / dist;
+                    c->pa[i] = ca[i] - om_gr[ga] * c->n[i];
+                    c->pb[i] = cb[i] + om_gr[gb] * c->n[i];
+                }
+                c->d = d; c->mu = P->mu_self;
+            }
+        }
+    }
+    return nc;
+}
+
+int om_contacts(const om_params* P, const double* st, double* out /* [MAXC][12] */) {
+    om_kin K;
+    om_contact C[MAXC];
+    fk(st, &K);
+    int nc = collide(P, &K, C);
+    for (int i = 0; i < nc; i++) {
+        double* o = out + 12 * i;
+        o[0] = C[i].la; o[1] = C[i].lb; o[2] = C[i].d; o[3] = C[i].mu;
+        for (int k = 0; k < 3; k++) { o[4 + k] = C[i].pa[k]; o[7 + k] = C[i].n[k]; }
+        o[10] = 0; o[11] = 0;
+    }
+    return nc;
+}
+
+static void plane_space(const double* n, double* p, double* q) { /* btPlaneSpace1 */
+    if (fabs(n[2]) > 0.7071067811865475244) {
+        double a = n[1] * n[1] + n[2] * n[2], k = 1.0 / sqrt(a);
+        p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
+        q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
+    } else {
+        double a = n[0] * n[0] + n[1] * n[1], k = 1.0 / sqrt(a);
+        p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
+        q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
+    }
+}
+
+/* --------------------------------------------------------------------------- one substep */
+typedef struct {
+    double J[NV], MiJ[NV];
+    double meff, b, lo, hi, lam;
+    int kind;  /* 0 limit, 1 normal, 2 friction */
+    int normal_row;
+    double mu;
+} om_row;
+
+static void substep(const om_params* P, double* st, const double* tau, int* ncontact_out) {
+    const double dt = P->dt;
+    om_kin K;
+    fk(st, &K);
+    om_contact C[MAXC];
+    int nc = collide(P, &K, C);
+    if (ncontact_out) *ncontact_out = nc;
+
+    /* 1. unconstrained dynamics -> nu* */
+    double acc[NV], nu[NV];
+    aba(P, st, &K, tau, acc);
+    for (int i = 0; i < 3; i++) { nu[i] = st[10 + i] + dt * acc[i]; nu[3 + i] = st[7 + i] + dt * acc[3 + i]; }
+    for (int j = 0; j < OM_ND; j++) nu[6 + j] = st[30 + j] + dt * acc[6 + j];
+    for (int a = 0; a < NV; a++) nu[a] = clampd(nu[a], -P->max_coord_vel, P->max_coord_vel);
+
+    /* 2. constraint rows */
+    static om_row rows[MAXROW];
+    int nr = 0;
+    double H[NV * NV];
+    mass_matrix(&K, H);
+    if (P->joint_damping)   /* constraint responses see the same implicit-damping inertia as the ABA */
+        for (int j = 0; j < OM_ND; j++) H[(6 + j) * NV + 6 + j] += dt * om_jdamp[j];
+    cholesky(H, NV);
+    for (int j = 0; j < OM_ND; j++) {  /* joint limits: lower then upper */
+        double q = st[13 + j];
+        for (int side = 0; side < 2; side++) {
+            double pen = side == 0 ? q - om_lo[j] : om_hi[j] - q;
+            if (pen > 0) continue;
+            om_row* r = &rows[nr++];
+            memset(r->J, 0, sizeof r->J);
+            r->J[6 + j] = side == 0 ? 1.0 : -1.0;
+            r->kind = 0; r->lo = 0; r->hi = P->limit_max_impulse;
+            r->b = -pen * P->erp_limit / dt;
+        }
+    }
+    int first_normal = nr;
+    double Jp[3 * NV], Jq[3 * NV];
+    for (int k = 0; k < nc; k++) {
+        om_contact* c = &C[k];
+        point_jacobian(&K, c->la, c->pa, Jp);
+        if (c->lb >= 0) {
+            point_jacobian(&K, c->lb, c->pb, Jq);
+            for (int i = 0; i < 3 * NV; i++) Jp[i] -= Jq[i];
+        }
+        om_row* r = &rows[nr++];
+        for (int a = 0; a < NV; a++) r->J[a] = c->n[0] * Jp[a] + c->n[1] * Jp[NV + a] + c->n[2] * Jp[2 * NV + a];
+        r->kind = 1; r->lo = 0; r->hi = 1e10;
+        r->b = c->d > 0 ? -c->d / dt : -c->d * P->erp_contact / dt;
+        r->mu = c->mu;
+    }
+    int first_fric = nr;
+    for (int k = 0; k < nc; k++) {
+        om_contact* c = &C[k];
+        point_jacobian(&K, c->la, c->pa, Jp);
+        if (c->lb >= 0) {
+            point_jacobian(&K, c->lb, c->pb, Jq);
+            for (int i = 0; i < 3 * NV; i++) Jp[i] -= Jq[i];
+        }
+        double vrel[3] = {0, 0, 0};
+        for (int i = 0; i < 3; i++)
+            for (int a = 0; a < NV; a++) vrel[i] += Jp[i * NV + a] * nu[a];
+        double vn = dot3(vrel, c->n), lat[3], t1[3], t2[3];
+        for (int i = 0; i < 3; i++) lat[i] = vrel[i] - c->n[i] * vn;
+        double l2 = dot3(lat, lat);
+        if (l2 > 1e-12) {
+            double il = 1.0 / sqrt(l2);
+            for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
+            cross(t1, c->n, t2);
+        } else {
+            plane_space(c->n, t1, t2);
+        }
+        for (int f = 0; f < 2; f++) {
+            const double* t = f == 0 ? t1 : t2;
+            om_row* r = &rows[nr++];
+            for (int a = 0; a < NV; a++) r->J[a] = t[0] * Jp[a] + t[1] * Jp[NV + a] + t[2] * Jp[2 * NV + a];
+            r->kind = 2; r->b = 0; r->mu = c->mu; r->normal_row = first_normal + k;
+            r->lo = 0; r->hi = 0;
+        }
+    }
+    (void)first_fric;
+    for (int i = 0; i < nr; i++) {
+        memcpy(rows[i].MiJ, rows[i].J, sizeof rows[i].J);
+        chol_solve(H, NV, rows[i].MiJ);
+        double s = 0;
+        for (int a = 0; a < NV; a++) s += rows[i].J[a] * rows[i].MiJ[a];
+        rows[i].meff = 1.0 / s;
+        rows[i].lam = 0;
+    }
+    /* 3. PGS */
+    for (int it = 0; it < P->iters; it++) {
+        for (int i = 0; i < nr; i++) {
+            om_row* r = &rows[i];
+            if (r->kind == 2) {
+                double ln = rows[r->normal_row].lam;
+                r->lo = -r->mu * ln;
+                r->hi = r->mu * ln;
+            }
+            double Jv = 0;
+            for (int a = 0; a < NV; a++) Jv += r->J[a] * nu[a];
+            double lnew = clampd(r->lam + r->meff * (r->b - Jv), r->lo, r->hi);
+            double dl = lnew - r->lam;
+            r->lam = lnew;
+            for (int a = 0; a < NV; a++) nu[a] += r->MiJ[a] * dl;
+        }
+    }
+    /* 4. integrate */
+    for (int i = 0; i < 3; i++) { st[10 + i] = nu[i]; st[7 + i] = nu[3 + i]; st[i] += dt * nu[3 + i]; }
+    for (int j = 0; j < OM_ND; j++) { st[30 + j] = nu[6 + j]; st[13 + j] += dt * nu[6 + j]; }
+    {
+        const double* w = st + 10;
+        double ang = norm3(w), ax[3];
+        if (ang * dt > 0.25 * M_PI) ang = 0.25 * M_PI / dt;   /* ANGULAR_MOTION_THRESHOLD */
+        if (ang < 0.001) {
+            double s = 0.5 * dt - dt * dt * dt * 0.020833333333 * ang * ang;
+            for (int i = 0; i < 3; i++) ax[i] = w[i] * s;
+        } else {
+            double s = sin(0.5 * ang * dt) / ang;
+            for (int i = 0; i < 3; i++) ax[i] = w[i] * s;
+        }
+        double dw = cos(0.5 * ang * dt);
+        double* q = st + 3; /* x y z w */
+        double nq[4] = {dw * q[0] + ax[0] * q[3] + ax[1] * q[2] - ax[2] * q[1],
+                        dw * q[1] + ax[1] * q[3] + ax[2] * q[0] - ax[0] * q[2],
+                        dw * q[2] + ax[2] * q[3] + ax[0] * q[1] - ax[1] * q[0],
+                        dw * q[3] - ax[0] * q[0] - ax[1] * q[1] - ax[2] * q[2]};
+        double nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+        for (int i = 0; i < 4; i++) q[i] = nq[i] / nn;
+    }
+}
+
+/* ------------------------------------------------------------------------- public API */
+void om_default_params(om_params* P) {
+    P->dt = 0.0165 / 4.0;
+    P->nsub = 4;
+    P->gravity = 9.8;
+    P->iters = 5;
+    P->erp_contact = 0.9;
+    P->erp_limit = 0.2;
+    P->mu_ground = 2.0 * 0.8;
+    P->mu_self = 2.0 * 2.0;
+    P->contact_thresh = 0.02;
+    P->lin_damp = 0.04;
+    P->ang_damp = 0.04;
+    P->limit_max_impulse = 100.0;
+    P->max_contacts = 24;
+    P->self_collision = 1;
+    P->joint_damping = 1;
+    P->max_coord_vel = 100.0;
+}
+
+/* one env step of physics: state (47) in place; tau_motor[17] in dof order (already 0.41*power*clip(a)). */
+void om_step(const om_params* P, double* st, const double* tau_motor, int* ncontact_out) {
+    for (int s = 0; s < P->nsub; s++) substep(P, st, tau_motor, s == P->nsub - 1 ? ncontact_out : 0);
+}
+
+/* diagnostics used by tests: unconstrained accelerations (ABA) and mass-matrix-based accelerations */
+void om_aba(const om_params* P, const double* st, const double* tau, double* acc) {
+    om_kin K;
+    fk(st, &K);
+    aba(P, st, &K, tau, acc);
+}
+void om_mass_matrix(const double* st, double* H) {
+    om_kin K;
+    fk(st, &K);
+    mass_matrix(&K, H);
+}
+void om_link_frames(const double* st, double* R, double* x) {
+    om_kin K;
+    fk(st, &K);
+    memcpy(R, K.R, sizeof K.R);
+    memcpy(x, K.x, sizeof K.x);
+}
+int om_nv(void) { return NV; }

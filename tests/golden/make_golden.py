@@ -1,0 +1,304 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the REAL reference env module (run in the survey container only).
+
+The reference's `low_level_env.py` and `humanoid.py` are imported unmodified from /root/reference with
+stub modules standing in for the absent third-party packages (gym, pybullet, pybullet_envs, ray):
+
+* `pybullet_envs...HumanoidBulletEnv(robot=...)` -> `FakeFlatEnv`, whose physics is the fp64 oracle
+  (`oracle/physics_oracle.c`) and whose `robot` is the reference's own `CustomHumanoidRobot`
+  (so `apply_action`, humanoid.py:54-60, runs from the reference source);
+* `WalkerBase.calc_state` (pybullet_envs, absent) is restated in `oracle/oracle.py::calc_state`;
+* the env's unseeded `np.random.default_rng()` (low_level_env.py:84) is replaced by a recording wrapper
+  around the counter-based lane RNG, so every draw is reproducible by the oracle and the kernel.
+
+Each scenario records, per step: the physics state before/after the step, the torques the reference
+applied, and every reference output (obs, reward, done, frame, bookkeeping).  Output:
+`tests/golden/golden_low.npz` (data only - no reference source is stored).
+
+Usage: python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(REPO, "imitation-learning-rl_amd"))
+import oracle as O  # noqa: E402
+from ilrl_amd.clips import load_clip  # noqa: E402
+
+CSV_DIR = os.path.join(REF, "Joints CSV With Hand")
+PART_NAMES = [p["name"] for p in O.LINKS["parts"]]
+
+# ----------------------------------------------------------------------------------- stub modules
+_state = {"env": None}
+
+
+def _mod(name, **kw):
+    m = types.ModuleType(name)
+    m.__dict__.update(kw)
+    sys.modules[name] = m
+    return m
+
+
+class Box:
+    def __init__(self, low=None, high=None, shape=None, dtype=np.float32):
+        self.low, self.high, self.shape = low, high, tuple(shape) if shape is not None else None
+
+
+class FakeJoint:
+    def __init__(self, env, dof):
+        self.env, self.dof = env, dof
+
+    def set_state(self, x, vx):
+        self.env.state[13 + self.dof] = x
+        self.env.state[30 + self.dof] = vx
+
+    def get_position(self):
+        return float(self.env.state[13 + self.dof])
+
+    def get_velocity(self):
+        return float(self.env.state[30 + self.dof])
+
+    def set_motor_torque(self, torque):
+        self.env.torque[self.dof] = torque
+
+
+class FakePart:
+    def __init__(self, env, idx):
+        self.env, self.idx = env, idx
+
+    def get_position(self):
+        return O.parts(self.env.state)[self.idx].copy()
+
+
+class FakePose:
+    def __init__(self, env):
+        self.env = env
+
+    def rpy(self):
+        return O.euler_from_quaternion(self.env.state[3:7])
+
+    def xyz(self):
+        return self.env.state[0:3].copy()
+
+
+class FakeBody:
+    def __init__(self, env):
+        self.env = env
+
+    def reset_position(self, p):
+        self.env.state[0:3] = p
+
+    def reset_orientation(self, q):
+        self.env.state[3:7] = q
+
+    def reset_velocity(self, linearVelocity=(0, 0, 0), angularVelocity=(0, 0, 0)):
+        self.env.state[7:10] = linearVelocity
+        self.env.state[10:13] = angularVelocity
+
+    def pose(self):
+        return FakePose(self.env)
+
+
+class WalkerBase:
+    """Stub of pybullet_envs.robot_locomotors.WalkerBase (attributes the reference touches)."""
+
+    def __init__(self, fn, robot_name, action_dim, obs_dim, power):
+        self.power = power
+        self.walk_target_x, self.walk_target_y = 1e3, 0
+        self.initial_z = None
+
+    def robot_specific_reset(self, bullet_client):
+        self.initial_z = None
+
+    def calc_state(self):
+        env = self.flat
+        obs, body_xyz, js, jal, rpy = O.calc_state(env.state, (self.walk_target_x, self.walk_target_y),
+                                                  initial_z=self.initial_z)
+        self.body_xyz, self.joint_speeds, self.joints_at_limit = body_xyz, js, jal
+        return obs
+
+
+class FakeScene:
+    def __init__(self, env):
+        self.env = env
+
+    def global_step(self):
+        self.env.state = O.phys_step(self.env.state, self.env.torque)
+        self.env.torque_log.append(self.env.torque.copy())
+        self.env.torque[:] = 0
+
+
+class FakeFlatEnv:
+    def __init__(self, robot=None):
+        self.robot = robot
+        robot.flat = self
+        self.state = np.zeros(47)
+        self.state[6] = 1
+        self.torque = np.zeros(17)
+        self.torque_log = []
+        self.jdict = {n: FakeJoint(self, i) for i, n in enumerate(O.DOF_NAMES)}
+        self.parts = {n: FakePart(self, i) for i, n in enumerate(PART_NAMES)}
+        self.scene = FakeScene(self)
+        self.action_space = Box(-1, 1, (17,))
+        robot.robot_body = FakeBody(self)
+        robot.jdict = self.jdict
+        robot.parts = self.parts
+
+    def reset(self):
+        # restoreState(): saved initial state (zero velocities); robot_specific_reset re-randomises
+        # joints in +-0.1 (all overwritten by resetFromFrame) and sets the motor table.
+        self.state[:] = 0
+        self.state[2] = 1.4
+        self.state[6] = 1
+        self.robot.robot_specific_reset(None)
+        return self.robot.calc_state()
+
+
+def install_stubs():
+    _mod("gym", Env=object)
+    _mod("gym.spaces", Box=Box, Discrete=object, Tuple=object)
+    sys.modules["gym"].spaces = sys.modules["gym.spaces"]
+    _mod("pybullet", addUserDebugLine=lambda *a, **k: 0, GEOM_HEIGHTFIELD=9)
+    _mod("pybullet_data", getDataPath=lambda: "")
+    _mod("pybullet_envs")
+    _mod("pybullet_envs.gym_locomotion_envs", HumanoidBulletEnv=lambda robot=None: FakeFlatEnv(robot))
+    _mod("pybullet_envs.robot_locomotors", WalkerBase=WalkerBase)
+    _mod("pybullet_envs.env_bases", MJCFBaseBulletEnv=object)
+    _mod("pybullet_envs.scene_abstract", Scene=object)
+    _mod("pybullet_envs.robot_bases", BodyPart=object)
+    _mod("ray")
+    _mod("ray.rllib")
+    _mod("ray.rllib.env", MultiAgentEnv=object)
+    import pandas as pd
+    orig = pd.read_csv
+
+    def read_csv(path, *a, **k):   # redirect the hard-coded ~/GitHub/TA path (low_level_env.py:58)
+        return orig(os.path.join(CSV_DIR, os.path.basename(str(path))), *a, **k)
+
+    pd.read_csv = read_csv
+    sys.path.insert(0, REF)
+
+
+class RecordingRNG:
+    def __init__(self, seed, lane):
+        self.r = O.LaneRNG(seed, lane)
+        self.log = []
+
+    def integers(self, lo, hi):
+        v = self.r.integers(lo, hi)
+        self.log.append((lo, hi, v))
+        return v
+
+
+BOOK = ["frame", "cur_timestep", "highLevelDegTarget", "lowTargetScore", "deltaJoints", "deltaVelJoints",
+        "bodyPostureScore", "electricityScore", "jointLimitScore", "aliveReward", "delta_lowTargetScore",
+        "predefinedTargetIndex"]
+VEC = ["target", "starting_robot_pos", "robot_pos", "starting_ep_pos"]
+
+
+def snapshot(env):
+    d = {k: float(getattr(env, k)) for k in BOOK}
+    for k in VEC:
+        d[k] = np.array(getattr(env, k), dtype=np.float64).copy()
+    d["walk_target"] = np.array([env.flat_env.robot.walk_target_x, env.flat_env.robot.walk_target_y], dtype=np.float64)
+    d["rng_counter"] = float(env.rng.r.counter)
+    return d
+
+
+def run_scenario(name, clip, seed, lane, steps, act_seed, act_scale=1.0, reset_yaw=0, start_frame=None,
+                 debug=False, teleport=None, predefined=None, timestep_offset=0):
+    import low_level_env
+    from humanoid import CustomHumanoidRobot
+    env = low_level_env.LowLevelHumanoidEnv(reference_name=clip, customRobot=CustomHumanoidRobot())
+    env.rng = RecordingRNG(seed, lane)
+    if predefined is not None:
+        env.usePredefinedTarget = True
+        env.predefinedTarget = np.array(predefined, dtype=np.float64)
+    if start_frame is None:
+        obs0 = env.reset(resetYaw=reset_yaw)
+    else:
+        obs0 = env.resetFromFrame(startFrame=start_frame, resetYaw=reset_yaw)
+    rec = {"obs0": np.array(obs0, dtype=np.float64), "state0": env.flat_env.state.copy()}
+    s0 = snapshot(env)
+    for k, v in s0.items():
+        rec["book0_" + k] = np.asarray(v)
+    if timestep_offset:
+        env.cur_timestep += timestep_offset
+    arng = np.random.default_rng(act_seed)
+    out = {k: [] for k in ["action", "state_pre", "state_post", "torque", "obs", "reward", "done", "teleported",
+                           "cur_timestep_pre"]}
+    books = []
+    for t in range(steps):
+        a = (arng.uniform(-1, 1, 17) * act_scale).astype(np.float32)
+        tele = 0
+        if teleport is not None and t in teleport:
+            # inject a base position near the current target (exercises checkTarget / done-by-distance)
+            off = teleport[t]
+            st = env.flat_env.state
+            st[0] = env.target[0] + off[0]
+            st[1] = env.target[1] + off[1]
+            tele = 1
+        out["cur_timestep_pre"].append(env.cur_timestep)
+        out["state_pre"].append(env.flat_env.state.copy())
+        obs, r, done, _ = env.step(a, debug=debug)
+        out["action"].append(a)
+        out["state_post"].append(env.flat_env.state.copy())
+        out["torque"].append(env.flat_env.torque_log[-1])
+        out["obs"].append(np.array(obs, dtype=np.float64))
+        out["reward"].append(float(r))
+        out["done"].append(bool(done))
+        out["teleported"].append(tele)
+        books.append(snapshot(env))
+        if done:
+            break
+    for k, v in out.items():
+        rec[k] = np.array(v)
+    for k in books[0]:
+        rec["book_" + k] = np.array([b[k] for b in books])
+    rec["meta"] = np.array([seed, lane, act_seed, int(debug), reset_yaw, -1 if start_frame is None else start_frame,
+                            timestep_offset], dtype=np.int64)
+    rec["clip"] = np.array(clip)
+    rec["draws"] = np.array(env.rng.log, dtype=np.int64).reshape(-1, 3)
+    rec["predefined"] = np.array(predefined if predefined is not None else np.zeros((0, 3)), dtype=np.float64)
+    print("%-26s %s steps=%3d done=%s draws=%d frame_end=%d" % (name, clip, len(out["reward"]), out["done"][-1],
+                                                               len(env.rng.log), int(rec["book_frame"][-1])))
+    return {name + "/" + k: v for k, v in rec.items()}
+
+
+def main():
+    install_stubs()
+    allrec = {}
+    S = []
+    for i, clip in enumerate(["motion02_04", "motion08_03", "motion09_03"]):
+        for lane in range(3):
+            S.append(dict(name="%s_l%d" % (clip, lane), clip=clip, seed=7, lane=lane, steps=60, act_seed=100 + 10 * i + lane))
+    # motion13_13: keep frames below the 120-row velocity table (the reference raises IndexError beyond it)
+    S.append(dict(name="motion13_13_f10", clip="motion13_13", seed=3, lane=0, steps=40, act_seed=5, start_frame=10))
+    S.append(dict(name="motion13_13_f60", clip="motion13_13", seed=3, lane=1, steps=25, act_seed=6, start_frame=60))
+    S.append(dict(name="yaw45_scaled", clip="motion09_03", seed=11, lane=0, steps=40, act_seed=9, reset_yaw=45, act_scale=1.7))
+    S.append(dict(name="debug_true", clip="motion08_03", seed=12, lane=0, steps=60, act_seed=10, debug=True, start_frame=0))
+    S.append(dict(name="teleport_target", clip="motion09_03", seed=13, lane=0, steps=30, act_seed=11,
+                  teleport={3: (0.2, -0.1), 9: (0.3, 0.3), 15: (-0.45, 0.1), 21: (0.0, 0.5)}))
+    S.append(dict(name="teleport_far", clip="motion08_03", seed=14, lane=0, steps=10, act_seed=12,
+                  teleport={4: (9.0, 0.0)}))
+    S.append(dict(name="predefined_course", clip="motion08_03", seed=15, lane=0, steps=30, act_seed=13, start_frame=0,
+                  debug=True, predefined=[[0, 5, 0], [5, 5, 0], [5, 0, 0], [0, 0, 0]],
+                  teleport={2: (0.1, 0.1), 8: (-0.2, 0.0), 14: (0.0, 0.3)}))
+    S.append(dict(name="timestep_limit", clip="motion02_04", seed=16, lane=0, steps=6, act_seed=14, start_frame=5,
+                  timestep_offset=2996))
+    S.append(dict(name="frame_wrap", clip="motion09_03", seed=17, lane=0, steps=12, act_seed=15, start_frame=84))
+    for s in S:
+        name = s.pop("name")
+        allrec.update(run_scenario(name, **s))
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden_low.npz")
+    np.savez_compressed(out, **allrec)
+    print("wrote", out, os.path.getsize(out), "bytes")
+
+
+if __name__ == "__main__":
+    main()
