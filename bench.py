@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""Benchmark: env steps/s of the HIP humanoid imitation env (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 4096 lanes per GPU, low-level imitation on motion02_04, uniform
+random actions in [-1,1] (pre-generated pool, device resident), auto-reset of done lanes inside the
+step launch.  A "step" = one hum_step launch advancing every lane one env step (4 physics substeps +
+observation + imitation reward + bookkeeping).  Multi-GPU: one process per GPU, lanes sharded by rank
+(global lane ids -> identical per-lane streams regardless of N), no data-path collective -> weak scaling.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "imitation-learning-rl_amd"))
+
+# algorithmic HBM bytes per env-step of the step kernel (DESIGN.md "Roofline"): reads + writes the
+# kernel must do per lane: physics state 47 f32 (r+w), bookkeeping 29 f64 + 8 i32 read / 29 f64 + 8 i32
+# written, action 17 f32, obs 70 f32, reward f32, done u8, frame i32.
+BYTES_PER_STEP_FP32 = 2 * 47 * 4 + 2 * (29 * 8 + 8 * 4) + 17 * 4 + 70 * 4 + 4 + 1 + 4
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--lanes", type=int, default=4096, help="env lanes per GPU")
+    ap.add_argument("--clip", default="motion02_04")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--block", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0 = min(16, cpus))")
+    return ap.parse_args()
+
+
+def _cpu_worker(args):
+    """Oracle (CPU restatement, fp64 C physics + numpy env logic) stepping for ~`seconds`."""
+    seconds, seed = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as O
+    from ilrl_amd.clips import load_clip
+    clip = load_clip("motion02_04")
+    env = O.OracleLowLevelEnv(clip, seed=seed, lane=0)
+    env.reset()
+    rng = np.random.default_rng(seed)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, _, d, _ = env.step(rng.uniform(-1, 1, 17).astype(np.float32))
+        n += 1
+        if d:
+            env.reset()
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds, workers):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(seconds, 1000 + w) for w in range(workers)])
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": "oracle/ (fp64 C physics restatement + numpy env logic; PyBullet absent) on motion02_04, "
+                      "%d processes x %.0f s of uniform-random-action steps with resets (%d steps)" % (workers, seconds, steps)}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    from ilrl_amd.vec_env import HumanoidVecEnv
+
+    n = a.lanes
+    env = HumanoidVecEnv(n, clips=(a.clip,), seed=0, device=local, lane_offset=rank * n, precision=a.precision,
+                         block_size=a.block)
+    env.reset()
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = [(torch.rand(n, 17, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
+    for w in range(a.warmup):
+        env.step(pool[w % 16], autoreset=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for s in range(a.steps):
+        env.step(pool[s % 16], autoreset=True)
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / a.steps            # average launch duration on the launch stream
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    flags = env.error_flags()
+    if rank == 0:
+        total = n * world * a.steps
+        value = total / wall_max
+        bpl = BYTES_PER_STEP_FP32 if a.precision == "fp32" else BYTES_PER_STEP_FP32 + 2 * 47 * 4
+        achieved = n * bpl / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        tp = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tp):
+            try:
+                tj = json.load(open(tp))
+                key = "%s_%d_%s" % (a.clip, n, a.precision)
+                if key in tj:
+                    traffic = tj[key]["bytes_per_launch"]
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "env steps/sec at N parallel humanoids (4096 per MI355X), motion02_04 low-level imitation",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": wall_max / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
+            "config": {"workload": "HumanoidBulletEnv-v0-Low step+reward, %s, %d envs/GPU, uniform random actions, "
+                                   "auto-reset" % (a.clip, n), "envs_per_gpu": n, "clip": a.clip,
+                       "parallelism": "lane-sharded x%d" % world, "block": a.block},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_env_step": bpl, "kernel_ms": kern_ms},
+            "error_flags": flags,
+        }
+        if world == 1 and a.cpu_seconds > 0:
+            workers = a.cpu_workers or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, workers)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

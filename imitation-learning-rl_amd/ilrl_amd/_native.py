@@ -1,0 +1,102 @@
+"""ctypes binding of the C-ABI in include/humanoid_env.h (libhumenv.so, built for gfx950).
+
+The product path has NO CPU fallback: if the HIP library is missing this module raises on use.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
+
+HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 32, 12
+HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS = 1, 2
+HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
+HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW = 1, 2, 4
+
+# bookkeeping layout (HUM_BK_*)
+BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, target=4, starting_robot_pos=7,
+          robot_pos=10, starting_ep_pos=13, highLevelDegTarget=16, walk_target=17, lowTargetScore=19,
+          deltaJoints=20, deltaVelJoints=21, bodyPostureScore=22, electricityScore=23, jointLimitScore=24,
+          aliveReward=25, delta_lowTargetScore=26, clip=27, mode=28, rng_key_lo=29, rng_key_hi=30)
+AUX = ["deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bodyPostureScore", "highTargetScore",
+       "driftScore", "baseReward", "aliveReward", "electricityScore", "jointLimitScore", "dist_from_origin"]
+
+# every symbol include/humanoid_env.h declares
+EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_create", "hum_destroy", "hum_set_clip",
+           "hum_set_lane_clips", "hum_set_lane_modes", "hum_set_predefined_targets", "hum_reset", "hum_step",
+           "hum_step_graph", "hum_get_aux", "hum_get_state", "hum_set_state", "hum_get_parts",
+           "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream"]
+
+
+class HumConfig(ctypes.Structure):
+    _fields_ = [("n_lanes", ctypes.c_int32), ("device", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("lane_offset", ctypes.c_int64), ("precision", ctypes.c_int32), ("block_size", ctypes.c_int32),
+                ("dt_env", ctypes.c_double), ("substeps", ctypes.c_int32), ("gravity", ctypes.c_double),
+                ("solver_iters", ctypes.c_int32), ("erp_contact", ctypes.c_double), ("erp_limit", ctypes.c_double),
+                ("mu_ground", ctypes.c_double), ("mu_self", ctypes.c_double), ("contact_thresh", ctypes.c_double),
+                ("lin_damp", ctypes.c_double), ("ang_damp", ctypes.c_double),
+                ("limit_max_impulse", ctypes.c_double), ("max_coord_vel", ctypes.c_double),
+                ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
+                ("joint_damping", ctypes.c_int32)]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libhumenv.so (raises if the HIP extension was not built - there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError("HIP library %s not found: build it with `make -C imitation-learning-rl_amd/csrc` "
+                          "or __graft_entry__.build()" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.hum_abi_version.restype = ctypes.c_int
+    L.hum_last_error.restype = ctypes.c_char_p
+    L.hum_default_config.argtypes = [ctypes.POINTER(HumConfig)]
+    L.hum_default_config.restype = None
+    L.hum_create.argtypes = [ctypes.POINTER(HumConfig), ctypes.POINTER(vp)]
+    L.hum_destroy.argtypes = [vp]
+    L.hum_set_clip.argtypes = [vp, i32, dp, i32, dp, i32, dp, i32, dp, i32]
+    L.hum_set_lane_clips.argtypes = [vp, vp]
+    L.hum_set_lane_modes.argtypes = [vp, vp]
+    L.hum_set_predefined_targets.argtypes = [vp, dp, i32]
+    L.hum_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.hum_step.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, vp]
+    L.hum_step_graph.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, i32]
+    L.hum_get_aux.argtypes = [vp, vp, vp]
+    L.hum_get_state.argtypes = [vp, dp, dp]
+    L.hum_set_state.argtypes = [vp, dp, dp]
+    L.hum_get_parts.argtypes = [vp, dp]
+    L.hum_get_error_flags.argtypes = [vp, ctypes.POINTER(u32)]
+    L.hum_sync.argtypes = [vp]
+    L.hum_num_lanes.argtypes = [vp]
+    L.hum_num_lanes.restype = i32
+    L.hum_stream.argtypes = [vp]
+    L.hum_stream.restype = vp
+    for name in EXPORTS:
+        getattr(L, name)  # AttributeError if the library lacks a declared symbol
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        raise NativeError("%s failed (%d): %s" % (what, rc, lib().hum_last_error().decode()))
+
+
+def default_config(**kw):
+    c = HumConfig()
+    lib().hum_default_config(ctypes.byref(c))
+    for k, v in kw.items():
+        if not hasattr(c, k):
+            raise TypeError("unknown hum_config field %r" % k)
+        setattr(c, k, v)
+    return c

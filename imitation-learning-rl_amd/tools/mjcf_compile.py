@@ -277,6 +277,18 @@ def compile_model(xml_path):
                 continue
             pairs.append([ga, gb])
 
+    # mass-carrying pybullet links (body link + merged fixed children), each with its own mass properties
+    # (Bullet's per-link velocity damping acts link by link, btMultiBody m_linearDamping/m_angularDamping)
+    mlinks = []
+    for bi, b in enumerate(mj):
+        if not b["geoms"]:
+            continue
+        ai = xf[bi][0]
+        props = [_geom_mass_props({"type": "sphere" if g["type"] == 0 else "capsule", "r": g["r"], "p1": g["p1"],
+                                   "p2": g["p2"]}) for g in geoms if g["mj"] == bi]
+        m, c, I = _combine(props)
+        mlinks.append({"name": b["name"], "body": ai, "mass": m, "com": c, "inertia": I})
+
     dof_index = {d["name"]: i for i, d in enumerate(dofs)}
     actions = [{"name": n, "dof": dof_index[n], "power": p, "gain": POWER * p} for n, p in MOTORS]
 
@@ -297,6 +309,8 @@ def compile_model(xml_path):
         "parts": [{"name": p["name"], "body": p["body"], "p": fl(p["p"])} for p in parts],
         "pairs": pairs,
         "actions": actions,
+        "links": [{"name": L["name"], "body": L["body"], "mass": float(L["mass"]), "com": fl(L["com"]),
+                   "inertia": fl(L["inertia"])} for L in mlinks],
     }
     return model
 
@@ -339,6 +353,12 @@ def emit_header(model, path):
     s.append(arr("pair_b", "int", [p[1] for p in model["pairs"]]))
     s.append(arr("part_body", "int", [p["body"] for p in P]))
     s.append(darr("part_p", [x for p in P for x in p["p"]]))
+    Lk = model["links"]
+    s.append("inline constexpr int NLINK = %d;\n" % len(Lk))
+    s.append(arr("link_body", "int", [L["body"] for L in Lk]))
+    s.append(darr("link_mass", [L["mass"] for L in Lk]))
+    s.append(darr("link_com", [x for L in Lk for x in L["com"]]))
+    s.append(darr("link_inertia", [x for L in Lk for x in L["inertia"]]))
     s.append(arr("act_dof", "int", [a["dof"] for a in model["actions"]]))
     s.append(darr("act_gain", [a["gain"] for a in model["actions"]]))
     s.append("}  // namespace hm\n")

@@ -1,0 +1,168 @@
+/* humanoid_env.h - C-ABI of the MI355X-native vectorised humanoid imitation environment.
+ *
+ * Drop-in boundary for the reference hot path `LowLevelHumanoidEnv.reset()/step()`
+ * (/root/reference/low_level_env.py:36-526, registered as "HumanoidBulletEnv-v0-Low" by
+ * train_config.py:29,321).  One handle = N independent env lanes resident on ONE GPU, advanced by one
+ * HIP kernel launch per env step.  The Python mirror (`ilrl_amd.low_level_env`) binds this header with
+ * ctypes; INTEGRATION.md shows the binding a maintainer adds on the reference side.
+ *
+ * Conventions
+ *   - extern "C", plain pointers + sizes, int status (0 = ok, < 0 = error, hum_last_error() for text);
+ *     no exceptions cross the ABI.
+ *   - Hot-path I/O (actions, obs, reward, done, frame) are DEVICE pointers on the handle's GPU (e.g.
+ *     torch.cuda tensors) - zero-copy.  State get/set use HOST pointers (bulk copies for parity tests).
+ *   - `stream` is a hipStream_t (NULL = the HIP null stream; hum_stream() returns the handle's own
+ *     stream).  Launches are asynchronous on that stream; state get/set, error flags and hum_sync
+ *     synchronise the device.  A handle is bound to one device and is not thread-safe.
+ *   - Lane physics state (47 doubles, HUM_NSTATE): base pos[3] (COM, world), base quat[4] (x,y,z,w),
+ *     base lin vel[3] (world), base ang vel[3] (world), q[17], qd[17]; dofs in MJCF order
+ *     abdomen_z, abdomen_y, abdomen_x, right_hip_x, right_hip_z, right_hip_y, right_knee, left_hip_x,
+ *     left_hip_z, left_hip_y, left_knee, right_shoulder_y, right_shoulder_x, right_elbow,
+ *     left_shoulder_y, left_shoulder_x, left_elbow  (== WalkerBase.ordered_joints, obs order).
+ *   - Actions: float32 [n,17] in CustomHumanoidRobot motor order (humanoid.py:28-37).
+ *   - Observation: float32 [n,70] = calc_state (42) ++ 14 x (relative target, target velocity)
+ *     (low_level_env.py:307-320).
+ */
+#ifndef HUMANOID_ENV_H
+#define HUMANOID_ENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HUM_ABI_VERSION 1
+#define HUM_NSTATE 47   /* physics state per lane */
+#define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
+#define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
+#define HUM_NBOOK 32    /* bookkeeping doubles per lane, layout HUM_BK_* below */
+#define HUM_NAUX 12     /* RewardLogCallback terms per lane, layout HUM_AUX_* below */
+#define HUM_MAX_CLIPS 8
+
+/* status codes */
+#define HUM_OK 0
+#define HUM_ERR_ARG -1
+#define HUM_ERR_HIP -2
+#define HUM_ERR_NOCLIP -3
+#define HUM_ERR_STATE -4
+
+/* hum_step flags */
+#define HUM_STEP_AUTORESET 1u     /* reset done lanes inside the same launch (obs_reset receives the new obs) */
+#define HUM_STEP_SKIP_PHYSICS 2u  /* treat the current physics state as post-step (parity: injected physics) */
+
+/* per-lane mode bits (hum_set_lane_modes) */
+#define HUM_MODE_DEBUG 1u         /* step(action, debug=True): done only on fall (low_level_env.py:470-471) */
+#define HUM_MODE_PREDEFINED 2u    /* usePredefinedTarget (low_level_env.py:253-255, 419-421) */
+
+/* error flag bits (hum_get_error_flags) */
+#define HUM_EFLAG_NONFINITE_ACTION 1u   /* humanoid.py:55 assert np.isfinite(a).all(): lane not stepped */
+#define HUM_EFLAG_VEL_ROW 2u            /* frame beyond the velocity table (motion13_13): clamped row used */
+#define HUM_EFLAG_CONTACT_OVERFLOW 4u   /* more contact candidates than max_contacts */
+
+/* bookkeeping layout (doubles; integers stored exactly) */
+enum {
+    HUM_BK_FRAME = 0, HUM_BK_TIMESTEP, HUM_BK_RNG_COUNTER, HUM_BK_PRED_INDEX,
+    HUM_BK_TARGET /* 3 */ = 4, HUM_BK_START_ROBOT_POS = 7, HUM_BK_ROBOT_POS = 10, HUM_BK_START_EP_POS = 13,
+    HUM_BK_HL_DEG_TARGET = 16, HUM_BK_WALK_TARGET /* 2 */ = 17, HUM_BK_LOW_TARGET_SCORE = 19,
+    HUM_BK_DELTA_JOINTS = 20, HUM_BK_DELTA_VEL_JOINTS = 21, HUM_BK_BODY_POSTURE = 22, HUM_BK_ELECTRICITY = 23,
+    HUM_BK_JOINT_LIMIT = 24, HUM_BK_ALIVE = 25, HUM_BK_DELTA_LOW_TARGET = 26, HUM_BK_CLIP = 27,
+    HUM_BK_MODE = 28,
+    /* 64-bit RNG stream key as two u32 halves; initialised to splitmix64(seed + lane_offset + lane) */
+    HUM_BK_RNG_KEY_LO = 29, HUM_BK_RNG_KEY_HI = 30
+};
+
+/* aux (RewardLogCallback, custom_callback.py:43-80) layout, float32 */
+enum {
+    HUM_AUX_DELTA_JOINTS = 0, HUM_AUX_DELTA_END_POINTS, HUM_AUX_LOW_TARGET_SCORE, HUM_AUX_DELTA_VEL_JOINTS,
+    HUM_AUX_BODY_POSTURE, HUM_AUX_HIGH_TARGET_SCORE, HUM_AUX_DRIFT_SCORE, HUM_AUX_BASE_REWARD, HUM_AUX_ALIVE,
+    HUM_AUX_ELECTRICITY, HUM_AUX_JOINT_LIMIT, HUM_AUX_DIST_FROM_ORIGIN
+};
+
+typedef struct hum_env hum_env;
+
+typedef struct hum_config {
+    int32_t n_lanes;          /* env instances on this GPU */
+    int32_t device;           /* HIP device ordinal */
+    uint64_t seed;            /* counter-based RNG seed (replaces the unseeded default_rng, :84) */
+    int64_t lane_offset;      /* global id of lane 0 (RNG stream key) -> results independent of sharding */
+    int32_t precision;        /* 0 = fp32 physics (default), 1 = fp64 physics */
+    int32_t block_size;       /* threads per block (multiple of 64) */
+    /* physics (defaults = pybullet_envs HumanoidBulletEnv: World(gravity 9.8, timestep 0.0165/4, frame_skip 4),
+       numSolverIterations 5, setDefaultContactERP 0.9; see DESIGN.md for each choice) */
+    double dt_env;            /* 0.0165 */
+    int32_t substeps;         /* 4 */
+    double gravity;           /* 9.8 */
+    int32_t solver_iters;     /* 5 */
+    double erp_contact, erp_limit, mu_ground, mu_self, contact_thresh;
+    double lin_damp, ang_damp, limit_max_impulse, max_coord_vel;
+    int32_t max_contacts;     /* <= 24 */
+    int32_t self_collision;   /* 1 */
+    int32_t joint_damping;    /* 1 = implicit MJCF joint damping */
+} hum_config;
+
+/* Version / build info. */
+int hum_abi_version(void);
+const char* hum_last_error(void);
+
+/* Fill `cfg` with the reference defaults (n_lanes = 1, device 0, seed 0). */
+void hum_default_config(hum_config* cfg);
+
+/* Replaces LowLevelHumanoidEnv.__init__ (low_level_env.py:39-172) for n lanes. */
+int hum_create(const hum_config* cfg, hum_env** out);
+int hum_destroy(hum_env* env);
+
+/* Upload one clip's four reference tables (low_level_env.py:59-70), row-major float64, fixed column
+ * order: joints = rightHipX, rightHipY, rightHipZ, rightKnee, leftHipX, leftHipY, leftHipZ, leftKnee,
+ * rightShoulderX, rightShoulderY, rightElbow, leftShoulderX, leftShoulderY, leftElbow (14);
+ * end points = {LeftLeg, LeftFoot, RightLeg, RightFoot, Head, LeftForeArm, LeftHand, RightForeArm,
+ * RightHand} x {X,Y,Z} (27).  max_frame = n_pos - 1 (:80-82). */
+int hum_set_clip(hum_env* env, int32_t clip_id, const double* pos, int32_t n_pos, const double* vel, int32_t n_vel,
+                 const double* rel, int32_t n_rel, const double* ep, int32_t n_ep);
+/* clip id per lane (host array of n_lanes); default all 0 */
+int hum_set_lane_clips(hum_env* env, const int32_t* clip_of_lane);
+/* per-lane HUM_MODE_* bits (host array of n_lanes) */
+int hum_set_lane_modes(hum_env* env, const uint32_t* modes);
+/* shared predefined target course (env_check.py:104-116): n x 3 float64 */
+int hum_set_predefined_targets(hum_env* env, const double* xyz, int32_t n);
+
+/* reset()/resetFromFrame() (low_level_env.py:224-305) for lanes with lane_mask[i] != 0 (device u8, NULL = all).
+ * start_frame (device i32, NULL = draw from the lane RNG as reset() does), reset_yaw_deg (device f64, NULL = 0).
+ * obs_out: device float32 [n,70] (rows of unmasked lanes untouched). */
+int hum_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+              float* obs_out, void* stream);
+
+/* step(action) (low_level_env.py:475-526) for all lanes: device float32 actions [n,17] ->
+ * obs [n,70] f32, reward [n] f32, done [n] u8, frame [n] i32 (frame may be NULL).
+ * With HUM_STEP_AUTORESET, done lanes are reset in the same launch; their post-reset observation is
+ * written to obs_reset (device [n,70], may be NULL) while `obs` keeps the terminal observation. */
+int hum_step(hum_env* env, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
+             uint32_t flags, float* obs_reset, void* stream);
+
+/* Capture `k` consecutive steps (same buffers, same flags) in a hipGraph and replay it on the handle's
+ * own stream (hum_stream()); inputs must be ready (synchronise the producing stream first). */
+int hum_step_graph(hum_env* env, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
+                   uint32_t flags, float* obs_reset, int32_t k);
+
+/* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
+int hum_get_aux(hum_env* env, float* aux_out, void* stream);
+
+/* Synchronous state access (host float64): phys [n,47], book [n,HUM_NBOOK]; either may be NULL. */
+int hum_get_state(hum_env* env, double* phys, double* book);
+int hum_set_state(hum_env* env, const double* phys, const double* book);
+
+/* Parts positions (33 x 3, pybullet parts dict order incl. 'floor') per lane, host float64 [n,33,3]. */
+int hum_get_parts(hum_env* env, double* parts);
+
+/* Sticky error bits (HUM_EFLAG_*) accumulated by kernels since the last call; synchronises. */
+int hum_get_error_flags(hum_env* env, uint32_t* flags);
+
+int hum_sync(hum_env* env);
+int32_t hum_num_lanes(const hum_env* env);
+/* hipStream_t of the handle (as void*) */
+void* hum_stream(hum_env* env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HUMANOID_ENV_H */

@@ -1,0 +1,243 @@
+"""GPU parity: the HIP kernel (through the C-ABI) vs the reference's golden vectors and the CPU oracle.
+
+Every golden scenario (tests/golden/make_golden.py, produced by the real reference env module) is
+replayed as ONE launch with one lane per recorded step: lane t gets the recorded physics state and the
+bookkeeping the reference held before step t, and the recorded action.
+
+* injected physics (HUM_STEP_SKIP_PHYSICS): lane physics = the reference's post-step state -> the
+  kernel's env logic (obs, reward, done, frame, target, ...) must equal the reference's;
+* full physics: lane physics = pre-step state -> kernel physics vs the fp64 oracle physics.
+
+Tolerances (stated per quantity below): done / frame / timestep / target decisions bit-exact;
+fp64 kernel: obs within 1 float32 ulp, reward 1e-9; fp32 kernel: obs 2e-5, reward 1e-4 (fp32 FK).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import scenarios
+from golden_replay import rec
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from ilrl_amd import _native as N  # noqa: E402
+from ilrl_amd.clips import load_clip  # noqa: E402
+from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+SCEN = ["motion02_04_l0", "motion02_04_l1", "motion02_04_l2", "motion08_03_l0", "motion08_03_l1", "motion08_03_l2",
+        "motion09_03_l0", "motion09_03_l1", "motion09_03_l2", "motion13_13_f10", "motion13_13_f60", "yaw45_scaled",
+        "debug_true", "teleport_target", "teleport_far", "predefined_course", "timestep_limit", "frame_wrap"]
+
+
+def book_rows(r, t_idx):
+    """HUM_NBOOK rows holding the reference bookkeeping BEFORE each step t in t_idx."""
+    seed, lane, _, debug, _, _, _ = [int(x) for x in r["meta"]]
+    key = O.splitmix64((seed + lane) & O.M64)
+    out = np.zeros((len(t_idx), N.HUM_NBOOK))
+    for row, t in enumerate(t_idx):
+        src = (lambda k: r["book0_" + k]) if t == 0 else (lambda k: r["book_" + k][t - 1])
+        b = out[row]
+        b[N.BK["frame"]] = src("frame")
+        b[N.BK["cur_timestep"]] = r["cur_timestep_pre"][t]
+        b[N.BK["rng_counter"]] = src("rng_counter")
+        b[N.BK["predefinedTargetIndex"]] = src("predefinedTargetIndex")
+        for k in ("target", "starting_robot_pos", "robot_pos", "starting_ep_pos"):
+            b[N.BK[k]:N.BK[k] + 3] = src(k)
+        b[N.BK["walk_target"]:N.BK["walk_target"] + 2] = src("walk_target")
+        for k in ("highLevelDegTarget", "lowTargetScore", "deltaJoints", "deltaVelJoints", "bodyPostureScore",
+                  "electricityScore", "jointLimitScore", "aliveReward", "delta_lowTargetScore"):
+            b[N.BK[k]] = src(k)
+        b[N.BK["clip"]] = 0
+        b[N.BK["mode"]] = (N.HUM_MODE_DEBUG if debug else 0) | (N.HUM_MODE_PREDEFINED if len(r["predefined"]) else 0)
+        b[N.BK["rng_key_lo"]] = key & 0xFFFFFFFF
+        b[N.BK["rng_key_hi"]] = key >> 32
+    return out
+
+
+def run_scenario(r, precision, skip_physics):
+    T = len(r["reward"])
+    env = HumanoidVecEnv(T, clips=(str(r["clip"]),), precision=precision)
+    if len(r["predefined"]):
+        env.set_predefined_targets(r["predefined"])
+    phys = r["state_post"] if skip_physics else r["state_pre"]
+    env.set_state(phys, book_rows(r, range(T)))
+    obs, rew, done, frame = env.step(r["action"], skip_physics=skip_physics)
+    out = dict(obs=obs.cpu().numpy(), rew=rew.cpu().numpy(), done=done.cpu().numpy().astype(bool),
+               frame=frame.cpu().numpy())
+    out["phys"], out["book"] = env.get_state()
+    env.close()
+    return out
+
+
+def f32_ulp_diff(a, b):
+    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b)
+
+
+@pytest.mark.parametrize("name", SCEN)
+def test_env_logic_matches_reference_fp64(golden, name):
+    """Injected physics, fp64 kernel: env logic equals the reference's golden outputs."""
+    r = rec(golden, name)
+    o = run_scenario(r, "fp64", skip_physics=True)
+    np.testing.assert_array_equal(o["done"], r["done"])
+    np.testing.assert_array_equal(o["frame"], r["book_frame"].astype(np.int32))
+    np.testing.assert_array_equal(o["book"][:, N.BK["cur_timestep"]], r["book_cur_timestep"])
+    np.testing.assert_array_equal(o["book"][:, N.BK["rng_counter"]], r["book_rng_counter"])
+    assert f32_ulp_diff(o["obs"], r["obs"]).max() <= 1, "obs beyond 1 float32 ulp"
+    np.testing.assert_allclose(o["rew"], r["reward"], rtol=1e-6, atol=1e-6)   # f32 output of an f64 sum
+    for k in ("target", "starting_robot_pos"):
+        np.testing.assert_allclose(o["book"][:, N.BK[k]:N.BK[k] + 3], r["book_" + k], rtol=0, atol=1e-12, err_msg=k)
+    np.testing.assert_allclose(o["book"][:, N.BK["robot_pos"]:N.BK["robot_pos"] + 3], r["book_robot_pos"], atol=1e-12)
+    for k in ("lowTargetScore", "deltaJoints", "deltaVelJoints", "bodyPostureScore", "electricityScore",
+              "jointLimitScore", "aliveReward", "delta_lowTargetScore", "highLevelDegTarget"):
+        np.testing.assert_allclose(o["book"][:, N.BK[k]], r["book_" + k], rtol=1e-12, atol=1e-12, err_msg=k)
+
+
+@pytest.mark.parametrize("name", SCEN)
+def test_env_logic_matches_reference_fp32(golden, name):
+    """Injected physics, fp32 kernel (the benchmarked build): FK in fp32."""
+    r = rec(golden, name)
+    o = run_scenario(r, "fp32", skip_physics=True)
+    np.testing.assert_array_equal(o["done"], r["done"])
+    np.testing.assert_array_equal(o["frame"], r["book_frame"].astype(np.int32))
+    np.testing.assert_allclose(o["obs"], r["obs"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(o["rew"], r["reward"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(o["book"][:, N.BK["target"]:N.BK["target"] + 3], r["book_target"], atol=1e-5)
+
+
+@pytest.mark.parametrize("name", SCEN)
+def test_physics_fp64_matches_oracle(golden, name):
+    """Full step, fp64 kernel physics (world-frame ABA, merged multi-dof bodies) vs the fp64 oracle
+    (local-frame ABA over pybullet's 32-link layout, H^-1 J^T responses)."""
+    r = rec(golden, name)
+    o = run_scenario(r, "fp64", skip_physics=False)
+    err = np.abs(o["phys"] - r["state_post"])
+    assert err.max() < 1e-6, "max state err %.3g at %s" % (err.max(), np.unravel_index(err.argmax(), err.shape))
+    np.testing.assert_array_equal(o["done"], r["done"])
+    np.testing.assert_allclose(o["obs"], r["obs"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(o["rew"], r["reward"], rtol=1e-5, atol=1e-5)
+
+
+def test_physics_fp32_matches_oracle_statistics(golden):
+    """Full step, fp32 kernel physics vs fp64 oracle over every recorded step of every scenario."""
+    errs, rerr, dmis, n = [], [], 0, 0
+    for name in scenarios(golden):
+        r = rec(golden, name)
+        o = run_scenario(r, "fp32", skip_physics=False)
+        errs.append(np.abs(o["obs"] - r["obs"]).max(axis=1))
+        rerr.append(np.abs(o["rew"] - r["reward"]))
+        dmis += int((o["done"] != r["done"]).sum())
+        n += len(r["reward"])
+    errs, rerr = np.concatenate(errs), np.concatenate(rerr)
+    print("fp32 physics: steps=%d obs err p50=%.2e p99=%.2e max=%.2e; reward err p50=%.2e p99=%.2e; done mismatches=%d"
+          % (n, np.median(errs), np.percentile(errs, 99), errs.max(), np.median(rerr), np.percentile(rerr, 99), dmis))
+    assert np.median(errs) < 1e-3
+    assert np.percentile(rerr, 90) < 1e-2
+    assert dmis <= max(1, n // 100)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_reset_matches_oracle(precision):
+    """reset()/resetFromFrame with lane RNG draws: kernel vs oracle (low_level_env.py:224-305)."""
+    clip = load_clip("motion08_03")
+    n = 64
+    env = HumanoidVecEnv(n, clips=(clip,), seed=123, precision=precision)
+    yaw = np.linspace(-90, 90, n)
+    sf = np.where(np.arange(n) % 2 == 0, -1, np.arange(n) % clip.max_frame - 5).astype(np.int32)
+    sf = np.where(sf < 0, -1, np.abs(sf))
+    obs = env.reset(start_frame=torch.as_tensor(sf, device="cuda"), reset_yaw=torch.as_tensor(yaw, device="cuda"))
+    obs = obs.cpu().numpy()
+    phys, book = env.get_state()
+    tol = 1e-12 if precision == "fp64" else 1e-5
+    for i in range(n):
+        o = O.OracleLowLevelEnv(clip, seed=123, lane=i)
+        ref = o.reset(resetYaw=yaw[i]) if sf[i] < 0 else o.resetFromFrame(int(sf[i]), resetYaw=yaw[i])
+        assert book[i, N.BK["frame"]] == o.frame
+        np.testing.assert_allclose(book[i, N.BK["target"]:N.BK["target"] + 3], o.target, atol=1e-12)
+        np.testing.assert_allclose(phys[i], o.state, atol=tol * 10, rtol=1e-6)
+        np.testing.assert_allclose(obs[i], ref, atol=2e-5 if precision == "fp32" else 1e-6, rtol=1e-5)
+    env.close()
+
+
+def test_rollout_properties_at_scale():
+    """4096 lanes x 200 auto-reset steps (bench shape): finite, frames/timesteps consistent."""
+    n = 4096
+    env = HumanoidVecEnv(n, clips=("motion02_04",), seed=5)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    prev_t = np.zeros(n)
+    for t in range(200):
+        a = torch.rand(n, 17, device="cuda", generator=g) * 2 - 1
+        obs, rew, done, frame = env.step(a, autoreset=True)
+    torch.cuda.synchronize()
+    phys, book = env.get_state()
+    assert np.isfinite(phys).all() and torch.isfinite(obs).all() and torch.isfinite(rew).all()
+    fr = book[:, N.BK["frame"]]
+    assert (fr >= 0).all() and (fr < 297).all()
+    assert (book[:, N.BK["cur_timestep"]] <= 200).all()
+    assert (env.error_flags() & N.HUM_EFLAG_NONFINITE_ACTION) == 0
+    env.close()
+
+
+def test_graph_replay_equals_eager():
+    n = 256
+    e1 = HumanoidVecEnv(n, clips=("motion09_03",), seed=9)
+    e2 = HumanoidVecEnv(n, clips=("motion09_03",), seed=9)
+    e1.reset(); e2.reset()
+    a = (torch.rand(n, 17, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 2 - 1).contiguous()
+    for _ in range(8):
+        e1.step(a, autoreset=True)
+    torch.cuda.synchronize()
+    rc = N.lib().hum_step_graph(e2.h, N.ctypes.c_void_p(a.data_ptr()), N.ctypes.c_void_p(e2.obs.data_ptr()),
+                                N.ctypes.c_void_p(e2.reward.data_ptr()), N.ctypes.c_void_p(e2.done.data_ptr()),
+                                N.ctypes.c_void_p(e2.frame.data_ptr()), N.HUM_STEP_AUTORESET,
+                                N.ctypes.c_void_p(e2.obs_reset.data_ptr()), 8)
+    assert rc == 0
+    torch.cuda.synchronize()
+    p1, b1 = e1.get_state()
+    p2, b2 = e2.get_state()
+    np.testing.assert_array_equal(p1, p2)
+    np.testing.assert_array_equal(b1, b2)
+    e1.close(); e2.close()
+
+
+def test_nonfinite_action_flagged():
+    env = HumanoidVecEnv(4, clips=("motion09_03",))
+    env.reset()
+    a = torch.zeros(4, 17, device="cuda")
+    a[2, 5] = float("nan")
+    env.step(a)
+    assert env.error_flags() & N.HUM_EFLAG_NONFINITE_ACTION
+    assert env.done[2].item() == 1
+    env.close()
+
+
+def test_gym_view_and_vector_env():
+    from ilrl_amd.low_level_env import HumanoidVectorEnv, LowLevelHumanoidEnv
+    e = LowLevelHumanoidEnv(reference_name="motion09_03")
+    o = e.reset()
+    assert o.shape == (70,) and o.dtype == np.float64
+    o, r, d, info = e.step(np.zeros(17, np.float32))
+    assert isinstance(r, float) and isinstance(d, bool) and info == {}
+    assert e.cur_timestep == 1 and e.target.shape == (3,)
+    with pytest.raises(AssertionError):
+        e.step(np.full(17, np.nan, np.float32))
+    e.close()
+    v = HumanoidVectorEnv(8, reference_name="motion09_03")
+    obs = v.vector_reset()
+    assert len(obs) == 8
+    for _ in range(5):
+        obs, rews, dones, infos = v.vector_step(np.zeros((8, 17), np.float32))
+        for i, d in enumerate(dones):
+            if d:
+                assert v.reset_at(i).shape == (70,)
+    u = v.get_unwrapped()[0]
+    for attr in ("deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bodyPostureScore",
+                 "highTargetScore", "driftScore", "baseReward", "aliveReward", "electricityScore", "jointLimitScore",
+                 "robot_pos"):
+        getattr(u, attr)

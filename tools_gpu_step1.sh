@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU session script: parity tests, smoke, short bench.  Stops at the first crash/timeout.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 1200 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 5 > gpurun_out/bench.log 2>&1 || exit $?
+echo done
