@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--block", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0 = min(16, cpus))")
+    ap.add_argument("--phys", action="append", default=[], help="physics override k=v (hum_config field), diagnostics")
     return ap.parse_args()
 
 
@@ -85,8 +86,12 @@ def main():
     from ilrl_amd.vec_env import HumanoidVecEnv
 
     n = a.lanes
+    phys = {}
+    for kv in a.phys:
+        k, v = kv.split("=")
+        phys[k] = float(v) if "." in v else int(v)
     env = HumanoidVecEnv(n, clips=(a.clip,), seed=0, device=local, lane_offset=rank * n, precision=a.precision,
-                         block_size=a.block)
+                         block_size=a.block, **phys)
     env.reset()
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [(torch.rand(n, 17, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
@@ -135,7 +140,7 @@ def main():
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
             "config": {"workload": "HumanoidBulletEnv-v0-Low step+reward, %s, %d envs/GPU, uniform random actions, "
                                    "auto-reset" % (a.clip, n), "envs_per_gpu": n, "clip": a.clip,
-                       "parallelism": "lane-sharded x%d" % world, "block": a.block},
+                       "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_env_step": bpl, "kernel_ms": kern_ms},

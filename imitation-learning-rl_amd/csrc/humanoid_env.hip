@@ -14,6 +14,7 @@
 #include "../../include/humanoid_env.h"
 #include "physics.h"
 #include "envlogic.h"
+#include "physics_group.h"
 
 using namespace hk;
 
@@ -70,11 +71,7 @@ struct KArgs {
 };
 
 // ----------------------------------------------------------------------------------- SoA lane I/O
-template <typename T>
-__device__ inline void load_lane(const KArgs& a, int i, T* st, Book& b) {
-    const T* ph = (const T*)a.phys;
-#pragma unroll
-    for (int e = 0; e < HUM_NSTATE; e++) st[e] = ph[(long)e * a.n + i];
+__device__ inline void load_book(const KArgs& a, int i, Book& b) {
     const int* bi = a.bi;
     b.frame = bi[0 * a.n + i]; b.timestep = bi[1 * a.n + i]; b.pred_idx = bi[2 * a.n + i];
     b.clip = bi[3 * a.n + i]; b.rng_ctr = (unsigned)bi[4 * a.n + i]; b.mode = (unsigned)bi[5 * a.n + i];
@@ -86,10 +83,13 @@ __device__ inline void load_lane(const KArgs& a, int i, T* st, Book& b) {
     b.dj = D(16); b.dvj = D(17); b.bps = D(18); b.es = D(19); b.jls = D(20); b.alive = D(21); b.dlts = D(22);
 }
 template <typename T>
-__device__ inline void store_lane(const KArgs& a, int i, const T* st, const Book& b) {
-    T* ph = (T*)a.phys;
+__device__ inline void load_lane(const KArgs& a, int i, T* st, Book& b) {
+    const T* ph = (const T*)a.phys;
 #pragma unroll
-    for (int e = 0; e < HUM_NSTATE; e++) ph[(long)e * a.n + i] = st[e];
+    for (int e = 0; e < HUM_NSTATE; e++) st[e] = ph[(long)e * a.n + i];
+    load_book(a, i, b);
+}
+__device__ inline void store_book(const KArgs& a, int i, const Book& b) {
     int* bi = a.bi;
     bi[0 * a.n + i] = b.frame; bi[1 * a.n + i] = b.timestep; bi[2 * a.n + i] = b.pred_idx;
     bi[3 * a.n + i] = b.clip; bi[4 * a.n + i] = (int)b.rng_ctr; bi[5 * a.n + i] = (int)b.mode;
@@ -98,6 +98,13 @@ __device__ inline void store_lane(const KArgs& a, int i, const T* st, const Book
     for (int k = 0; k < 3; k++) { D(k) = b.target[k]; D(3 + k) = b.srp[k]; D(6 + k) = b.robot_pos[k]; D(9 + k) = b.sep[k]; }
     D(12) = b.hldt; D(13) = b.wt[0]; D(14) = b.wt[1]; D(15) = b.lts;
     D(16) = b.dj; D(17) = b.dvj; D(18) = b.bps; D(19) = b.es; D(20) = b.jls; D(21) = b.alive; D(22) = b.dlts;
+}
+template <typename T>
+__device__ inline void store_lane(const KArgs& a, int i, const T* st, const Book& b) {
+    T* ph = (T*)a.phys;
+#pragma unroll
+    for (int e = 0; e < HUM_NSTATE; e++) ph[(long)e * a.n + i] = st[e];
+    store_book(a, i, b);
 }
 
 __device__ inline int draw(const KArgs& a, int i, Book& b, int lo, int hi) {
@@ -173,47 +180,11 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
     ref_obs(c, b.frame, obs + 42, ef);
 }
 
-// ----------------------------------------------------------------------------------- step
+// Post-physics part of step (low_level_env.py:481-526) + optional auto-reset; stores state, book, outputs.
 template <typename T>
-__global__ void __launch_bounds__(256) step_kernel(KArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    T st[HUM_NSTATE];
-    Book b;
-    load_lane(a, i, st, b);
+__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef) {
     const ClipDev& c = a.clips[b.clip];
-    unsigned ef = 0;
-    float act[HUM_NACT];
-    bool finite = true;
-#pragma unroll
-    for (int k = 0; k < HUM_NACT; k++) {
-        act[k] = a.act[(long)i * HUM_NACT + k];
-        finite &= isfinite(act[k]);
-    }
     float obs[HUM_NOBS];
-    if (!finite) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
-        ef |= HUM_EFLAG_NONFINITE_ACTION;
-#pragma unroll
-        for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = 0.f;
-        a.rew[i] = 0.f;
-        a.done[i] = 1;
-        if (a.frame_out) a.frame_out[i] = b.frame;
-        atomicOr(a.eflags, ef);
-        return;
-    }
-    if (!(a.flags & HUM_STEP_SKIP_PHYSICS)) {
-        T tau[NDOF];
-#pragma unroll
-        for (int k = 0; k < HUM_NACT; k++) {   // apply_action: float(1 * power * 0.41 * clip(a)) in float32
-            const float g = (float)act_gain[k];
-            tau[act_dof[k]] = (T)(double)(g * fminf(fmaxf(act[k], -1.f), 1.f));
-        }
-        Lane<T> rows{(T*)a.scratch + i, (long)a.n};
-#pragma unroll 1
-        for (int s = 0; s < a.P.nsub; s++) {
-            if (substep(a.P, st, tau, rows)) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
-        }
-    }
     // calc_state (:481) and robot_pos (:483-486)
     float js[NDOF];
     int jal;
@@ -296,6 +267,99 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
         }
     }
     store_lane(a, i, st, b);
+    if (ef) atomicOr(a.eflags, ef);
+}
+
+
+// ----------------------------------------------------------------------------------- step
+template <typename T>
+__global__ void __launch_bounds__(256) step_kernel(KArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    T st[HUM_NSTATE];
+    Book b;
+    load_lane(a, i, st, b);
+    unsigned ef = 0;
+    float act[HUM_NACT];
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < HUM_NACT; k++) {
+        act[k] = a.act[(long)i * HUM_NACT + k];
+        finite &= isfinite(act[k]);
+    }
+    if (!finite) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
+        ef |= HUM_EFLAG_NONFINITE_ACTION;
+#pragma unroll
+        for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = 0.f;
+        a.rew[i] = 0.f;
+        a.done[i] = 1;
+        if (a.frame_out) a.frame_out[i] = b.frame;
+        atomicOr(a.eflags, ef);
+        return;
+    }
+    if (!(a.flags & HUM_STEP_SKIP_PHYSICS)) {
+        T tau[NDOF];
+#pragma unroll
+        for (int k = 0; k < HUM_NACT; k++) {   // apply_action: float(1 * power * 0.41 * clip(a)) in float32
+            const float g = (float)act_gain[k];
+            tau[act_dof[k]] = (T)(double)(g * fminf(fmaxf(act[k], -1.f), 1.f));
+        }
+        Lane<T> rows{(T*)a.scratch + i, (long)a.n};
+#pragma unroll 1
+        for (int s = 0; s < a.P.nsub; s++) {
+            if (substep(a.P, st, tau, rows)) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
+        }
+    }
+    post_step(a, i, st, b, act, ef);
+}
+
+// Cooperative step: 16 lanes per env, 4 envs per 64-thread block (one wavefront), env working set in LDS.
+template <typename T>
+__global__ void __launch_bounds__(64) step_group_kernel(KArgs a) {
+    __shared__ GroupLDS<T> sh[EPB];
+    const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
+    const int i = blockIdx.x * EPB + ge;
+    const bool valid = i < a.n;
+    GroupLDS<T>& S = sh[ge];
+    const ModelTab<T>& M = tab<T>();
+    for (int e = l; e < HUM_NSTATE; e += GL) {
+        T v = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
+        S.st[e] = v;
+        S.st0[e] = v;
+    }
+    bool fin = true;
+    for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60), float32 product
+        const float av = valid ? a.act[(long)i * HUM_NACT + k] : 0.f;
+        fin = fin && isfinite(av);
+        S.tau[M.act_dof[k]] = (T)(double)(M.act_gain[k] * fminf(fmaxf(isfinite(av) ? av : 0.f, -1.f), 1.f));
+    }
+    const int gbit = (threadIdx.x & 63) & ~(GL - 1);
+    const bool env_ok = ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
+    __syncthreads();
+    unsigned ef = 0;
+    if (!(a.flags & HUM_STEP_SKIP_PHYSICS)) {
+#pragma unroll 1
+        for (int s = 0; s < a.P.nsub; s++) group_substep(a.P, S, l, ef);
+    }
+    if (valid && l == 0) {
+        Book b;
+        load_book(a, i, b);
+        if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
+            ef |= HUM_EFLAG_NONFINITE_ACTION;
+            for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = 0.f;
+            a.rew[i] = 0.f;
+            a.done[i] = 1;
+            if (a.frame_out) a.frame_out[i] = b.frame;
+        } else {
+            T st[HUM_NSTATE];
+            float act[HUM_NACT];
+#pragma unroll
+            for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
+#pragma unroll
+            for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[(long)i * HUM_NACT + k];
+            post_step(a, i, st, b, act, ef);
+        }
+    }
     if (ef) atomicOr(a.eflags, ef);
 }
 
@@ -406,7 +470,7 @@ KArgs make_args(hum_env* e) {
     a.P.ang_damp = c.ang_damp;
     a.P.limit_max_impulse = c.limit_max_impulse;
     a.P.max_coord_vel = c.max_coord_vel;
-    a.P.max_contacts = c.max_contacts < MAXC ? c.max_contacts : MAXC;
+    a.P.max_contacts = c.max_contacts;
     a.P.self_collision = c.self_collision;
     a.P.joint_damping = c.joint_damping;
     for (int k = 0; k < HUM_MAX_CLIPS; k++) a.clips[k] = e->clips[k];
@@ -454,9 +518,10 @@ void hum_default_config(hum_config* c) {
     c->ang_damp = 0.04;
     c->limit_max_impulse = 100.0;
     c->max_coord_vel = 100.0;
-    c->max_contacts = 24;
+    c->max_contacts = 16;
     c->self_collision = 1;
     c->joint_damping = 1;
+    c->kernel = 1;
 }
 
 int hum_create(const hum_config* cfg, hum_env** out) {
@@ -466,6 +531,9 @@ int hum_create(const hum_config* cfg, hum_env** out) {
         return fail(HUM_ERR_ARG, "hum_create: block_size must be a multiple of 16 in [16, 256]");
     if (cfg->precision != 0 && cfg->precision != 1) return fail(HUM_ERR_ARG, "hum_create: precision must be 0 or 1");
     if (cfg->substeps <= 0 || cfg->solver_iters < 0) return fail(HUM_ERR_ARG, "hum_create: bad solver settings");
+    if (cfg->kernel != 0 && cfg->kernel != 1) return fail(HUM_ERR_ARG, "hum_create: kernel must be 0 (per-lane) or 1 (cooperative)");
+    if (cfg->max_contacts < 0 || cfg->max_contacts > (cfg->kernel == 1 ? MAXC_G : MAXC))
+        return fail(HUM_ERR_ARG, "hum_create: max_contacts out of range for the selected kernel");
     HIPCHK(hipSetDevice(cfg->device));
     hum_env* e = new hum_env();
     e->cfg = *cfg;
@@ -594,8 +662,14 @@ int hum_step(hum_env* e, const float* actions, float* obs, float* reward, uint8_
     a.flags = flags;
     a.obs_reset = obs_reset;
     hipStream_t s = stream_of(e, stream);
-    if (e->cfg.precision) hipLaunchKernelGGL(step_kernel<double>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
-    else hipLaunchKernelGGL(step_kernel<float>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
+    if (e->cfg.kernel == 1) {
+        const dim3 g((e->n + EPB - 1) / EPB), blk(EPB * GL);
+        if (e->cfg.precision) hipLaunchKernelGGL(step_group_kernel<double>, g, blk, 0, s, a);
+        else hipLaunchKernelGGL(step_group_kernel<float>, g, blk, 0, s, a);
+    } else {
+        if (e->cfg.precision) hipLaunchKernelGGL(step_kernel<double>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
+        else hipLaunchKernelGGL(step_kernel<float>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
+    }
     HIPCHK(hipGetLastError());
     return HUM_OK;
 }

@@ -1,0 +1,771 @@
+// physics_group.h - cooperative (16 lanes per env) version of the humanoid substep.
+//
+// MI355X mapping: a 64-lane wavefront = 4 envs x 16 lanes; each env's working set lives in LDS
+// (struct GroupLDS, ~17.6 KB fp32), so a CU holds 8 envs (2 blocks) with no scratch spills and a
+// compact instruction stream.  Same algorithm and operation order as physics.h (the per-lane kernel,
+// kept as the reference-shaped variant) except for the order of floating-point sums inside the
+// element-parallel ABA backward pass and the 16-lane DPP reductions of the PGS row products.
+//
+//   FK              every lane (registers), lane 0 publishes R/o/u to LDS
+//   ABA pass 1      lane b = body b: velocity, bias acceleration, spatial inertia, bias force
+//   ABA pass 2      body by body (leaves -> root), lanes split the 6k / k^2 / 21 matrix entries
+//   ABA pass 3      every lane redundantly (tiny), lane 0 publishes accelerations
+//   limits/contacts lane-parallel candidate tests, ballot-compacted in the oracle's order
+//   rows            one constraint row per lane: Jacobian + test-impulse response M^-1 J^T
+//   PGS             rows in Bullet order; J.nu over the 16 lanes by DPP row_ror reductions
+#pragma once
+#include "physics.h"
+
+namespace hk {
+
+constexpr int GL = 16;                       // lanes per env
+constexpr int EPB = 4;                       // envs per 64-thread block (one wavefront)
+constexpr int MAXC_G = 16;                   // contact cap of the cooperative kernel
+constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // 65 rows
+constexpr int RW = 2 * NV + 6;               // J[NV], M[NV], b, lo, hi, lam, meff, mu
+constexpr int NCAND_GROUND = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 1 : 2; return n; }();
+constexpr int NCAND = NCAND_GROUND + NPAIR;
+
+// generic (runtime-indexable) model tables in __constant__ memory
+template <typename T>
+struct ModelTab {
+    int parent[NB], dof0[NB], ndof[NB], nlink[NB], link0[NB];
+    T toff[NB][3], Roff[NB][9], mass[NB], com[NB][3], inertia[NB][9];
+    int onpath[NB][NB];          // onpath[b][x]: x is b or an ancestor of b (x >= 1)
+    int daxis[NDOF];
+    T dsign[NDOF], lo[NDOF], hi[NDOF], damp[NDOF];
+    T lmass[NLINK], lcom[NLINK][3], linertia[NLINK][9];
+    int gbody[NGEOM], gtype[NGEOM];
+    T gr[NGEOM], gp1[NGEOM][3], gp2[NGEOM][3];
+    int cand_a[NCAND], cand_b[NCAND];    // ground: (geom, endpoint) with cand_b = -1 - endpoint; pair: (ga, gb)
+    int act_dof[NACT];
+    float act_gain[NACT];
+};
+
+template <typename T>
+constexpr ModelTab<T> make_tab() {
+    ModelTab<T> m{};
+    for (int b = 0; b < NB; b++) {
+        m.parent[b] = body_parent[b]; m.dof0[b] = body_dof0[b]; m.ndof[b] = body_ndof[b];
+        m.mass[b] = (T)body_mass[b];
+        for (int i = 0; i < 3; i++) { m.toff[b][i] = (T)body_toff[3 * b + i]; m.com[b][i] = (T)body_com[3 * b + i]; }
+        for (int i = 0; i < 9; i++) { m.Roff[b][i] = (T)body_Roff[9 * b + i]; m.inertia[b][i] = (T)body_inertia[9 * b + i]; }
+        m.nlink[b] = 0; m.link0[b] = -1;
+        for (int x = 0; x < NB; x++) m.onpath[b][x] = 0;
+        for (int x = b; x > 0; x = body_parent[x]) m.onpath[b][x] = 1;
+    }
+    for (int l = 0; l < NLINK; l++) {
+        const int b = link_body[l];
+        if (m.link0[b] < 0) m.link0[b] = l;
+        m.nlink[b]++;
+        m.lmass[l] = (T)link_mass[l];
+        for (int i = 0; i < 3; i++) m.lcom[l][i] = (T)link_com[3 * l + i];
+        for (int i = 0; i < 9; i++) m.linertia[l][i] = (T)link_inertia[9 * l + i];
+    }
+    for (int d = 0; d < NDOF; d++) {
+        m.daxis[d] = dof_axis[d]; m.dsign[d] = (T)dof_sign[d]; m.lo[d] = (T)dof_lo[d]; m.hi[d] = (T)dof_hi[d];
+        m.damp[d] = (T)dof_damping[d];
+    }
+    int c = 0;
+    for (int g = 0; g < NGEOM; g++) {
+        m.gbody[g] = geom_body[g]; m.gtype[g] = geom_type[g]; m.gr[g] = (T)geom_r[g];
+        for (int i = 0; i < 3; i++) { m.gp1[g][i] = (T)geom_p1[3 * g + i]; m.gp2[g][i] = (T)geom_p2[3 * g + i]; }
+        for (int e = 0; e < (geom_type[g] == 0 ? 1 : 2); e++) { m.cand_a[c] = g; m.cand_b[c] = -1 - e; c++; }
+    }
+    for (int k = 0; k < NPAIR; k++) { m.cand_a[c] = pair_a[k]; m.cand_b[c] = pair_b[k]; c++; }
+    for (int k = 0; k < NACT; k++) { m.act_dof[k] = hm::act_dof[k]; m.act_gain[k] = (float)hm::act_gain[k]; }
+    return m;
+}
+
+__constant__ ModelTab<float> kTabF = make_tab<float>();
+__constant__ ModelTab<double> kTabD = make_tab<double>();
+template <typename T> __device__ inline const ModelTab<T>& tab();
+template <> __device__ inline const ModelTab<float>& tab<float>() { return kTabF; }
+template <> __device__ inline const ModelTab<double>& tab<double>() { return kTabD; }
+
+template <typename T>
+struct GroupLDS {
+    T st[HUM_NSTATE + 1];
+    T st0[HUM_NSTATE + 1];      // pre-step state (restored for lanes with a non-finite action)
+    T tau[NDOF + 3];
+    T nu[NV + 1];
+    T acc[NV + 1];
+    T R[NB][9], o[NB][3], u[NDOF][3];
+    T U[NDOF][6], Dinv[NB][9], L0[21], uu[NDOF];
+    T c[NB][6];
+    union {
+        struct {
+            T V[NB][6], IA[NB][21], pA[NB][6];
+            T W[3][6], D[9], pa[6];
+        } aba;
+        struct {
+            T gp[NGEOM][2][3];
+            T con[MAXC_G][12];
+            T row[MAXR_G][RW];
+            int rdesc[MAXR_G];   // limit rows: dof | side << 8
+        } cr;
+    } x;
+    int nl, nc, flag;
+};
+
+__device__ inline void wave_sync() {   // cross-lane LDS ordering inside one wavefront
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 16-lane (DPP row) all-reduce sum
+__device__ inline float row_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror:8
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror:4
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xF, 0xF, false));  // row_ror:2
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false));  // row_ror:1
+    return v;
+}
+template <int CTRL>
+__device__ inline double mov_dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ inline double row_sum(double v) {
+    v += mov_dpp_d<0x128>(v);
+    v += mov_dpp_d<0x124>(v);
+    v += mov_dpp_d<0x122>(v);
+    v += mov_dpp_d<0x121>(v);
+    return v;
+}
+
+// ------------------------------------------------------------------------- test-impulse response
+// Same algorithm as physics.h::impulse_response, reading the ABA factorisation from LDS.
+template <typename T>
+__device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int bb, const T* fb, int jd, T jsign,
+                                  T* out) {
+    T pA[NB][6];
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int e = 0; e < 6; e++) pA[b][e] = (b == ba ? -fa[e] : T(0)) - (b == bb ? fb[e] : T(0));
+    T uq[NDOF];
+#pragma unroll
+    for (int b = NB - 1; b >= 1; b--) {
+        const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
+#pragma unroll
+        for (int j = 0; j < k; j++) {
+            const int d = d0 + j;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[b], S.u[d], Sc + 3);
+            T s = (d == jd) ? jsign : T(0);
+#pragma unroll
+            for (int e = 0; e < 6; e++) s -= Sc[e] * pA[b][e];
+            uq[d] = s;
+        }
+        T w[3];
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+            T t = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) t += S.Dinv[b][3 * i + j] * uq[d0 + j];
+            w[i] = t;
+        }
+#pragma unroll
+        for (int e = 0; e < 6; e++) {
+            T s = pA[b][e];
+#pragma unroll
+            for (int i = 0; i < k; i++) s += S.U[d0 + i][e] * w[i];
+            pA[p][e] += s;
+        }
+    }
+    T a[NB][6];
+#pragma unroll
+    for (int e = 0; e < 6; e++) a[0][e] = -pA[0][e];
+    {
+        T L[21];
+#pragma unroll
+        for (int q = 0; q < 21; q++) L[q] = S.L0[q];
+        chol6_solve(L, a[0]);
+    }
+#pragma unroll
+    for (int e = 0; e < 6; e++) out[e] = a[0][e];
+#pragma unroll
+    for (int b = 1; b < NB; b++) {
+        const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
+        T r[3];
+#pragma unroll
+        for (int j = 0; j < k; j++) {
+            T s = uq[d0 + j];
+#pragma unroll
+            for (int e = 0; e < 6; e++) s -= S.U[d0 + j][e] * a[p][e];
+            r[j] = s;
+        }
+#pragma unroll
+        for (int e = 0; e < 6; e++) a[b][e] = a[p][e];
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+            T s = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) s += S.Dinv[b][3 * i + j] * r[j];
+            out[6 + d0 + i] = s;
+            const int d = d0 + i;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[b], S.u[d], Sc + 3);
+#pragma unroll
+            for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * s;
+        }
+    }
+}
+
+// J row for a spatial force f on body b (generic: runtime b)
+template <typename T>
+__device__ inline void g_row_jacobian(const GroupLDS<T>& S, int b, const T* f, T sgn, T* J) {
+    const ModelTab<T>& M = tab<T>();
+#pragma unroll
+    for (int e = 0; e < 6; e++) J[e] += sgn * f[e];
+#pragma unroll
+    for (int x = 1; x < NB; x++) {
+        const bool on = b >= 0 && M.onpath[b < 0 ? 0 : b][x];
+#pragma unroll
+        for (int k = 0; k < body_ndof[x]; k++) {
+            const int d = body_dof0[x] + k;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[x], S.u[d], Sc + 3);
+            T s = 0;
+#pragma unroll
+            for (int e = 0; e < 6; e++) s += f[e] * Sc[e];
+            if (on) J[6 + d] += sgn * s;
+        }
+    }
+}
+
+// spatial velocity of body b from the generalised velocity nu (LDS)
+template <typename T>
+__device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
+    const ModelTab<T>& M = tab<T>();
+#pragma unroll
+    for (int e = 0; e < 6; e++) V[e] = S.nu[e];
+#pragma unroll
+    for (int x = 1; x < NB; x++) {
+        const bool on = b >= 0 && M.onpath[b < 0 ? 0 : b][x];
+#pragma unroll
+        for (int k = 0; k < body_ndof[x]; k++) {
+            const int d = body_dof0[x] + k;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[x], S.u[d], Sc + 3);
+            const T qd = S.nu[6 + d];
+            if (on)
+#pragma unroll
+                for (int e = 0; e < 6; e++) V[e] += Sc[e] * qd;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------- one cooperative substep
+// Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
+template <typename T>
+__device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, unsigned& ef) {
+    const ModelTab<T>& M = tab<T>();
+    const T dt = (T)P.dt;
+    // ---- FK (every lane, registers); lane 0 publishes
+    {
+        T st[HUM_NSTATE];
+#pragma unroll
+        for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
+        Kin<T> K;
+        forward_kinematics(st + 3, st + 13, K);
+        if (l == 0) {
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+#pragma unroll
+                for (int i = 0; i < 9; i++) S.R[b][i] = K.R[b][i];
+#pragma unroll
+                for (int i = 0; i < 3; i++) S.o[b][i] = K.o[b][i];
+            }
+#pragma unroll
+            for (int d = 0; d < NDOF; d++)
+#pragma unroll
+                for (int i = 0; i < 3; i++) S.u[d][i] = K.u[d][i];
+        }
+        if (l < 16) {   // generalised velocity
+            S.nu[l] = l < 3 ? S.st[10 + l] : (l < 6 ? S.st[7 + l - 3] : S.st[30 + l - 6]);
+            if (l < NV - 16) S.nu[16 + l] = S.st[30 + 10 + l];
+        }
+    }
+    __syncthreads();
+    // ---- ABA pass 1: lane b = body b
+    if (l < NB) {
+        const int b = l;
+        T V[6];
+#pragma unroll
+        for (int e = 0; e < 6; e++) V[e] = S.nu[e];
+        // parent velocity: path excluding b itself
+#pragma unroll
+        for (int x = 1; x < NB; x++) {
+            const bool on = M.onpath[b][x] && x != b;
+#pragma unroll
+            for (int k = 0; k < body_ndof[x]; k++) {
+                const int d = body_dof0[x] + k;
+                T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+                cross3(S.o[x], S.u[d], Sc + 3);
+                if (on)
+#pragma unroll
+                    for (int e = 0; e < 6; e++) V[e] += Sc[e] * S.nu[6 + d];
+            }
+        }
+        T cb[6] = {0, 0, 0, 0, 0, 0};
+        const int k = M.ndof[b], d0 = M.dof0[b];
+        for (int j = 0; j < k; j++) {
+            const int d = d0 + j;
+            T Sq[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0}, cr[6];
+            cross3(S.o[b], S.u[d], Sq + 3);
+            const T qd = S.nu[6 + d];
+#pragma unroll
+            for (int e = 0; e < 6; e++) { Sq[e] *= qd; V[e] += Sq[e]; }
+            crm(V, Sq, cr);
+#pragma unroll
+            for (int e = 0; e < 6; e++) cb[e] += cr[e];
+        }
+        T Rb[9], ob[3];
+#pragma unroll
+        for (int i = 0; i < 9; i++) Rb[i] = S.R[b][i];
+#pragma unroll
+        for (int i = 0; i < 3; i++) ob[i] = S.o[b][i];
+        T c3[3], Icw[9], IA[21], h[6], pA[6];
+#pragma unroll
+        for (int i = 0; i < 3; i++) c3[i] = ob[i] + Rb[3 * i] * M.com[b][0] + Rb[3 * i + 1] * M.com[b][1] + Rb[3 * i + 2] * M.com[b][2];
+        {
+            T RI[9];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++)
+                    RI[3 * r + cc] = Rb[3 * r] * M.inertia[b][cc] + Rb[3 * r + 1] * M.inertia[b][3 + cc] + Rb[3 * r + 2] * M.inertia[b][6 + cc];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++) Icw[3 * r + cc] = RI[3 * r] * Rb[3 * cc] + RI[3 * r + 1] * Rb[3 * cc + 1] + RI[3 * r + 2] * Rb[3 * cc + 2];
+        }
+        spatial_inertia(M.mass[b], c3, Icw, IA);
+        symmv(IA, V, h);
+        crf(V, h, pA);
+        const T mg = -M.mass[b] * (T)P.gravity;
+        pA[0] -= c3[1] * mg;
+        pA[1] -= -c3[0] * mg;
+        pA[5] -= mg;
+        for (int q = 0; q < M.nlink[b]; q++) {   // Bullet per-link velocity damping
+            const int lk = M.link0[b] + q;
+            T cl[3], vc[3], Iw[9], wI[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) cl[i] = ob[i] + Rb[3 * i] * M.lcom[lk][0] + Rb[3 * i + 1] * M.lcom[lk][1] + Rb[3 * i + 2] * M.lcom[lk][2];
+            cross3(V, cl, vc);
+#pragma unroll
+            for (int i = 0; i < 3; i++) vc[i] += V[3 + i];
+            const T kv = (T)P.lin_damp * (T(1) + sqrt(dot3(vc, vc)));
+            const T kw = (T)P.ang_damp * (T(1) + sqrt(dot3(V, V)));
+            {
+                T RI[9];
+#pragma unroll
+                for (int r = 0; r < 3; r++)
+#pragma unroll
+                    for (int cc = 0; cc < 3; cc++)
+                        RI[3 * r + cc] = Rb[3 * r] * M.linertia[lk][cc] + Rb[3 * r + 1] * M.linertia[lk][3 + cc] + Rb[3 * r + 2] * M.linertia[lk][6 + cc];
+#pragma unroll
+                for (int r = 0; r < 3; r++)
+#pragma unroll
+                    for (int cc = 0; cc < 3; cc++) Iw[3 * r + cc] = RI[3 * r] * Rb[3 * cc] + RI[3 * r + 1] * Rb[3 * cc + 1] + RI[3 * r + 2] * Rb[3 * cc + 2];
+            }
+#pragma unroll
+            for (int i = 0; i < 3; i++) wI[i] = Iw[3 * i] * V[0] + Iw[3 * i + 1] * V[1] + Iw[3 * i + 2] * V[2];
+            const T m = M.lmass[lk];
+            T F[3], n[3], cxF[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) { F[i] = -m * vc[i] * kv; n[i] = -wI[i] * kw; }
+            cross3(cl, F, cxF);
+#pragma unroll
+            for (int i = 0; i < 3; i++) { pA[i] -= n[i] + cxF[i]; pA[3 + i] -= F[i]; }
+        }
+#pragma unroll
+        for (int e = 0; e < 6; e++) { S.x.aba.V[b][e] = V[e]; S.c[b][e] = cb[e]; S.x.aba.pA[b][e] = pA[e]; }
+#pragma unroll
+        for (int q = 0; q < 21; q++) S.x.aba.IA[b][q] = IA[q];
+    }
+    __syncthreads();
+    // ---- ABA pass 2: body by body, matrix entries split over the 16 lanes
+    auto& A = S.x.aba;
+#pragma unroll
+    for (int b = NB - 1; b >= 1; b--) {
+        const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
+        // U = IA S (6k entries) ; u = tau - S^T pA (k entries, lanes 16-k..15 reuse)
+        for (int q = l; q < 6 * k; q += GL) {
+            const int j = q / 6, r = q % 6, d = d0 + j;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[b], S.u[d], Sc + 3);
+            T s = 0;
+#pragma unroll
+            for (int f = 0; f < 6; f++) s += A.IA[b][sidx(r, f)] * Sc[f];
+            S.U[d][r] = s;
+        }
+        if (l < k) {
+            const int j = l, d = d0 + j;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[b], S.u[d], Sc + 3);
+            T sp = 0;
+#pragma unroll
+            for (int e = 0; e < 6; e++) sp += Sc[e] * A.pA[b][e];
+            T uj = S.tau[d] - sp;
+            if (P.joint_damping) uj -= M.damp[d] * S.nu[6 + d];
+            S.uu[d] = uj;
+        }
+        __syncthreads();
+        // D = S^T U (+ dt*damping), inverse by lane 0
+        if (l == 0) {
+            T D[9], Di[9];
+#pragma unroll
+            for (int i = 0; i < k; i++) {
+                const int d = d0 + i;
+                T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+                cross3(S.o[b], S.u[d], Sc + 3);
+#pragma unroll
+                for (int j = 0; j < k; j++) {
+                    T s = 0;
+#pragma unroll
+                    for (int e = 0; e < 6; e++) s += Sc[e] * S.U[d0 + j][e];
+                    D[3 * i + j] = s;
+                }
+                if (P.joint_damping) D[4 * i] += dt * M.damp[d];
+            }
+            if (k == 1) small_inverse<T, 1>(D, Di);
+            else if (k == 2) small_inverse<T, 2>(D, Di);
+            else small_inverse<T, 3>(D, Di);
+#pragma unroll
+            for (int q = 0; q < 9; q++) S.Dinv[b][q] = Di[q];
+        }
+        __syncthreads();
+        // W = U Dinv
+        for (int q = l; q < 6 * k; q += GL) {
+            const int j = q / 6, r = q % 6;
+            T s = 0;
+#pragma unroll
+            for (int i = 0; i < k; i++) s += S.U[d0 + i][r] * S.Dinv[b][3 * i + j];
+            A.W[j][r] = s;
+        }
+        __syncthreads();
+        // Ia = IA - W U^T (21 entries) ; IA_p += Ia
+#pragma unroll
+        for (int q0 = 0; q0 < 21; q0 += GL) {
+            const int q = q0 + l;
+            if (q < 21) {
+                int r = 0, cc = q;   // packed upper index -> (r, c)
+                while (cc >= 6 - r) { cc -= 6 - r; r++; }
+                cc += r;
+                T s = A.IA[b][q];
+#pragma unroll
+                for (int j = 0; j < k; j++) s -= A.W[j][r] * S.U[d0 + j][cc];
+                A.IA[b][q] = s;
+                A.IA[p][q] += s;
+            }
+        }
+        __syncthreads();
+        // pa = pA + Ia c + W u ; pA_p += pa
+        if (l < 6) {
+            T s = A.pA[b][l];
+#pragma unroll
+            for (int f = 0; f < 6; f++) s += A.IA[b][sidx(l, f)] * S.c[b][f];
+#pragma unroll
+            for (int j = 0; j < k; j++) s += A.W[j][l] * S.uu[d0 + j];
+            A.pA[p][l] += s;
+        }
+        __syncthreads();
+    }
+    // ---- base + pass 3 (redundant on every lane; lane 0 publishes)
+    {
+        T L[21], a[NB][6];
+        T IA0[21];
+#pragma unroll
+        for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q];
+        chol6(IA0, L);
+#pragma unroll
+        for (int e = 0; e < 6; e++) a[0][e] = -A.pA[0][e];
+        chol6_solve(L, a[0]);
+        T acc[NV];
+#pragma unroll
+        for (int b = 1; b < NB; b++) {
+            const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
+            T ap[6], r[3];
+#pragma unroll
+            for (int e = 0; e < 6; e++) ap[e] = a[p][e] + S.c[b][e];
+#pragma unroll
+            for (int j = 0; j < k; j++) {
+                T s = S.uu[d0 + j];
+#pragma unroll
+                for (int e = 0; e < 6; e++) s -= S.U[d0 + j][e] * ap[e];
+                r[j] = s;
+            }
+#pragma unroll
+            for (int e = 0; e < 6; e++) a[b][e] = ap[e];
+#pragma unroll
+            for (int i = 0; i < k; i++) {
+                T s = 0;
+#pragma unroll
+                for (int j = 0; j < k; j++) s += S.Dinv[b][3 * i + j] * r[j];
+                acc[6 + d0 + i] = s;
+                const int d = d0 + i;
+                T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+                cross3(S.o[b], S.u[d], Sc + 3);
+#pragma unroll
+                for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * s;
+            }
+        }
+        T nu0[6];
+#pragma unroll
+        for (int e = 0; e < 6; e++) nu0[e] = S.nu[e];
+        T wxv[3];
+        cross3(nu0, nu0 + 3, wxv);
+#pragma unroll
+        for (int i = 0; i < 3; i++) { acc[i] = a[0][i]; acc[3 + i] = a[0][3 + i] + wxv[i]; }
+        __syncthreads();   // everyone has read A.IA/pA (the union is reused below)
+        if (l == 0) {
+#pragma unroll
+            for (int q = 0; q < 21; q++) S.L0[q] = L[q];
+#pragma unroll
+            for (int e = 0; e < NV; e++) S.acc[e] = acc[e];
+        }
+    }
+    __syncthreads();
+    // ---- nu* = clamp(nu + dt acc)
+    {
+        const T vmax = (T)P.max_coord_vel;
+        S.nu[l] = clampT(S.nu[l] + dt * S.acc[l], -vmax, vmax);
+        if (l < NV - GL) S.nu[GL + l] = clampT(S.nu[GL + l] + dt * S.acc[GL + l], -vmax, vmax);
+    }
+    // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
+    auto& C = S.x.cr;
+    for (int g = l; g < NGEOM; g += GL) {
+        const int b = M.gbody[g];
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            C.gp[g][0][i] = S.o[b][i] + S.R[b][3 * i] * M.gp1[g][0] + S.R[b][3 * i + 1] * M.gp1[g][1] + S.R[b][3 * i + 2] * M.gp1[g][2];
+            C.gp[g][1][i] = S.o[b][i] + S.R[b][3 * i] * M.gp2[g][0] + S.R[b][3 * i + 1] * M.gp2[g][1] + S.R[b][3 * i + 2] * M.gp2[g][2];
+        }
+    }
+    const int gbit = (threadIdx.x & 63) & ~(GL - 1);   // first lane of this group in the wave
+    const unsigned long long lanemask_lt = (1ull << (threadIdx.x & 63)) - 1ull;
+    int nl = 0;
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++) {   // dofs 0..15, then dof 16 (lane 0)
+        const int d = rd * GL + l;
+        bool lowv = false, hiv = false;
+        if (d < NDOF) {
+            const T q = S.st[13 + d];
+            lowv = (q - M.lo[d]) <= 0;
+            hiv = (M.hi[d] - q) <= 0;
+        }
+        // each dof yields up to 2 rows (lower first); count per lane then prefix within the group
+        const int cnt = (int)lowv + (int)hiv;
+        const unsigned long long b1 = __ballot(cnt >= 1), b2 = __ballot(cnt >= 2);
+        const unsigned long long gm1 = (b1 >> gbit) & 0xFFFFull, gm2 = (b2 >> gbit) & 0xFFFFull;
+        const unsigned long long below = ((lanemask_lt >> gbit) & 0xFFFFull);
+        const int pos = nl + __popcll(gm1 & below) + __popcll(gm2 & below);
+        if (lowv) C.rdesc[pos] = d | (0 << 8);
+        if (hiv) C.rdesc[pos + (int)lowv] = d | (1 << 8);
+        nl += __popcll(gm1) + __popcll(gm2);
+    }
+    __syncthreads();
+    // ---- contacts: candidate c = 16*round + lane, compacted in candidate order
+    const int maxc = P.max_contacts < MAXC_G ? P.max_contacts : MAXC_G;
+    int nc = 0, over = 0;
+    const T basez = S.st[2];
+    for (int r0 = 0; r0 < NCAND; r0 += GL) {
+        const int c = r0 + l;
+        bool hit = false;
+        int ba = 0, bb = -1;
+        T pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
+        if (c < NCAND) {
+            const int ga = M.cand_a[c], gb = M.cand_b[c];
+            if (gb < 0) {   // ground point of geom ga, endpoint -1-gb
+                const int e = -1 - gb;
+                const T* p = C.gp[ga][e];
+                d = basez + p[2] - M.gr[ga];
+                hit = d < (T)P.contact_thresh;
+                ba = M.gbody[ga];
+                pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - M.gr[ga];
+                pb[0] = pa[0]; pb[1] = pa[1]; pb[2] = pa[2];
+            } else if (P.self_collision) {
+                T ca[3], cb[3], dv[3];
+                seg_seg(C.gp[ga][0], C.gp[ga][1], C.gp[gb][0], C.gp[gb][1], ca, cb);
+#pragma unroll
+                for (int i = 0; i < 3; i++) dv[i] = ca[i] - cb[i];
+                const T dist = sqrt(dot3(dv, dv));
+                const T ra = M.gr[ga], rb = M.gr[gb];
+                d = dist - ra - rb;
+                hit = d < (T)P.contact_thresh && dist > (T)1e-9;
+                if (hit) {
+                    const T idist = T(1) / dist;
+#pragma unroll
+                    for (int i = 0; i < 3; i++) {
+                        n[i] = dv[i] * idist;
+                        pa[i] = ca[i] - ra * n[i];
+                        pb[i] = cb[i] + rb * n[i];
+                    }
+                }
+                ba = M.gbody[ga];
+                bb = M.gbody[gb];
+            }
+        }
+        const unsigned long long bm = (__ballot(hit) >> gbit) & 0xFFFFull;
+        const int pos = nc + __popcll(bm & ((lanemask_lt >> gbit) & 0xFFFFull));
+        if (hit) {
+            if (pos < maxc) {
+                T* e = C.con[pos];
+                e[0] = (T)ba; e[1] = (T)bb;
+#pragma unroll
+                for (int i = 0; i < 3; i++) { e[2 + i] = pa[i]; e[5 + i] = pb[i]; e[8 + i] = n[i]; }
+                e[11] = d;
+            } else {
+                over = 1;
+            }
+        }
+        nc += __popcll(bm);
+    }
+    if (nc > maxc) { nc = maxc; over = 1; }
+    if (over) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
+    __syncthreads();
+    // ---- rows: one per lane (limits, normals, frictions), Jacobian + response
+    const int nrows = nl + 3 * nc;
+    for (int r = l; r < nrows; r += GL) {
+        T J[NV], Mi[NV];
+#pragma unroll
+        for (int e = 0; e < NV; e++) J[e] = 0;
+        T* R = C.row[r];
+        if (r < nl) {
+            const int d = C.rdesc[r] & 0xff, side = C.rdesc[r] >> 8;
+            const T sg = side == 0 ? T(1) : T(-1);
+            const T q = S.st[13 + d];
+            const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
+            g_response(S, -1, (const T*)nullptr, -1, (const T*)nullptr, d, sg, Mi);
+#pragma unroll
+            for (int e = 0; e < NV; e++) { R[e] = (e == 6 + d) ? sg : T(0); R[NV + e] = Mi[e]; }
+            R[2 * NV + 0] = -pen * (T)P.erp_limit / dt;
+            R[2 * NV + 1] = 0;
+            R[2 * NV + 2] = (T)P.limit_max_impulse;
+            R[2 * NV + 3] = 0;
+            R[2 * NV + 4] = T(1) / (sg * Mi[6 + d]);
+            R[2 * NV + 5] = 0;
+        } else {
+            const int cidx = r < nl + nc ? r - nl : (r - nl - nc) >> 1;
+            const int f = r < nl + nc ? 0 : 1 + ((r - nl - nc) & 1);
+            const T* e = C.con[cidx];
+            const int ba = (int)e[0], bb = (int)e[1];
+            const T pa[3] = {e[2], e[3], e[4]}, pb[3] = {e[5], e[6], e[7]}, n[3] = {e[8], e[9], e[10]};
+            const T d = e[11];
+            T dir[3];
+            if (f == 0) {
+                dir[0] = n[0]; dir[1] = n[1]; dir[2] = n[2];
+            } else {
+                T Va[6], Vb[6], va[3], vb[3] = {0, 0, 0}, vr[3];
+                g_body_vel(S, ba, Va);
+                cross3(Va, pa, va);
+#pragma unroll
+                for (int i = 0; i < 3; i++) va[i] += Va[3 + i];
+                if (bb >= 0) {
+                    g_body_vel(S, bb, Vb);
+                    cross3(Vb, pb, vb);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) vb[i] += Vb[3 + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 3; i++) vr[i] = va[i] - vb[i];
+                const T vn = dot3(vr, n);
+                T lat[3], t1[3], t2[3];
+#pragma unroll
+                for (int i = 0; i < 3; i++) lat[i] = vr[i] - n[i] * vn;
+                const T l2 = dot3(lat, lat);
+                if (l2 > (T)1e-12) {
+                    const T il = T(1) / sqrt(l2);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
+                    cross3(t1, n, t2);
+                } else {
+                    plane_space(n, t1, t2);
+                }
+#pragma unroll
+                for (int i = 0; i < 3; i++) dir[i] = f == 1 ? t1[i] : t2[i];
+            }
+            T fa[6], fb[6];
+            cross3(pa, dir, fa); fa[3] = dir[0]; fa[4] = dir[1]; fa[5] = dir[2];
+            cross3(pb, dir, fb);
+            fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
+            g_row_jacobian(S, ba, fa, T(1), J);
+            if (bb >= 0) g_row_jacobian(S, bb, fb, T(1), J);
+            g_response(S, ba, fa, bb, fb, -1, T(0), Mi);
+            T jm = 0;
+#pragma unroll
+            for (int q = 0; q < NV; q++) { R[q] = J[q]; R[NV + q] = Mi[q]; jm += J[q] * Mi[q]; }
+            R[2 * NV + 0] = f == 0 ? (d > 0 ? -d / dt : -d * (T)P.erp_contact / dt) : T(0);
+            R[2 * NV + 1] = 0;
+            R[2 * NV + 2] = (T)1e10;
+            R[2 * NV + 3] = 0;
+            R[2 * NV + 4] = T(1) / jm;
+            R[2 * NV + 5] = bb >= 0 ? (T)P.mu_self : (T)P.mu_ground;
+        }
+    }
+    __syncthreads();
+    // ---- PGS (lane l owns nu[l] and nu[16+l])
+    T n0 = S.nu[l], n1 = l < NV - GL ? S.nu[GL + l] : T(0);
+    for (int it = 0; it < P.iters; it++) {
+        for (int r = 0; r < nrows; r++) {
+            T* R = C.row[r];
+            if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
+                const T ln = C.row[nl + ((r - nl - nc) >> 1)][2 * NV + 3];
+                const T mu = R[2 * NV + 5];
+                R[2 * NV + 1] = -mu * ln;
+                R[2 * NV + 2] = mu * ln;
+            }
+            T part = R[l] * n0 + (l < NV - GL ? R[GL + l] * n1 : T(0));
+            const T jv = row_sum(part);
+            const T lam = R[2 * NV + 3];
+            const T lnew = clampT(lam + R[2 * NV + 4] * (R[2 * NV + 0] - jv), R[2 * NV + 1], R[2 * NV + 2]);
+            const T dl = lnew - lam;
+            wave_sync();
+            R[2 * NV + 3] = lnew;
+            n0 += R[NV + l] * dl;
+            if (l < NV - GL) n1 += R[NV + GL + l] * dl;
+            wave_sync();
+        }
+    }
+    S.nu[l] = n0;
+    if (l < NV - GL) S.nu[GL + l] = n1;
+    __syncthreads();
+    // ---- integrate (lanes split the state), lane 0 the quaternion
+    {
+        if (l < 3) { S.st[10 + l] = S.nu[l]; S.st[7 + l] = S.nu[3 + l]; S.st[l] += dt * S.nu[3 + l]; }
+        for (int j = l; j < NDOF; j += GL) { S.st[30 + j] = S.nu[6 + j]; S.st[13 + j] += dt * S.nu[6 + j]; }
+        if (l == 0) {
+            T w[3] = {S.nu[0], S.nu[1], S.nu[2]};
+            T ang = sqrt(dot3(w, w)), ax[3];
+            const T thr = (T)(0.25 * 3.14159265358979323846);
+            if (ang * dt > thr) ang = thr / dt;
+            if (ang < (T)0.001) {
+                const T s = (T)0.5 * dt - dt * dt * dt * (T)0.020833333333 * ang * ang;
+#pragma unroll
+                for (int i = 0; i < 3; i++) ax[i] = w[i] * s;
+            } else {
+                const T s = sin((T)0.5 * ang * dt) / ang;
+#pragma unroll
+                for (int i = 0; i < 3; i++) ax[i] = w[i] * s;
+            }
+            const T dw = cos((T)0.5 * ang * dt);
+            T q[4] = {S.st[3], S.st[4], S.st[5], S.st[6]};
+            T nq[4] = {dw * q[0] + ax[0] * q[3] + ax[1] * q[2] - ax[2] * q[1],
+                       dw * q[1] + ax[1] * q[3] + ax[2] * q[0] - ax[0] * q[2],
+                       dw * q[2] + ax[2] * q[3] + ax[0] * q[1] - ax[1] * q[0],
+                       dw * q[3] - ax[0] * q[0] - ax[1] * q[1] - ax[2] * q[2]};
+            const T nn = T(1) / sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+#pragma unroll
+            for (int i = 0; i < 4; i++) S.st[3 + i] = nq[i] * nn;
+        }
+    }
+    __syncthreads();
+}
+
+}  // namespace hk

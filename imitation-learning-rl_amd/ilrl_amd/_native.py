@@ -37,7 +37,7 @@ class HumConfig(ctypes.Structure):
                 ("lin_damp", ctypes.c_double), ("ang_damp", ctypes.c_double),
                 ("limit_max_impulse", ctypes.c_double), ("max_coord_vel", ctypes.c_double),
                 ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
-                ("joint_damping", ctypes.c_int32)]
+                ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32)]
 
 
 class NativeError(RuntimeError):

@@ -96,9 +96,10 @@ typedef struct hum_config {
     int32_t solver_iters;     /* 5 */
     double erp_contact, erp_limit, mu_ground, mu_self, contact_thresh;
     double lin_damp, ang_damp, limit_max_impulse, max_coord_vel;
-    int32_t max_contacts;     /* <= 24 */
+    int32_t max_contacts;     /* 16 (cooperative kernel <= 16, per-lane kernel <= 24) */
     int32_t self_collision;   /* 1 */
     int32_t joint_damping;    /* 1 = implicit MJCF joint damping */
+    int32_t kernel;           /* 1 = cooperative (16 lanes/env, LDS-resident; default), 0 = one env per lane */
 } hum_config;
 
 /* Version / build info. */

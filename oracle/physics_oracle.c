@@ -675,7 +675,7 @@ void om_default_params(om_params* P) {
     P->lin_damp = 0.04;
     P->ang_damp = 0.04;
     P->limit_max_impulse = 100.0;
-    P->max_contacts = 24;
+    P->max_contacts = 16;
     P->self_collision = 1;
     P->joint_damping = 1;
     P->max_coord_vel = 100.0;

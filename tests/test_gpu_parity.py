@@ -58,9 +58,9 @@ def book_rows(r, t_idx):
     return out
 
 
-def run_scenario(r, precision, skip_physics):
+def run_scenario(r, precision, skip_physics, kernel=1):
     T = len(r["reward"])
-    env = HumanoidVecEnv(T, clips=(str(r["clip"]),), precision=precision)
+    env = HumanoidVecEnv(T, clips=(str(r["clip"]),), precision=precision, kernel=kernel)
     if len(r["predefined"]):
         env.set_predefined_targets(r["predefined"])
     phys = r["state_post"] if skip_physics else r["state_pre"]
@@ -79,11 +79,12 @@ def f32_ulp_diff(a, b):
     return np.abs(a - b)
 
 
+@pytest.mark.parametrize("kernel", [1, 0])
 @pytest.mark.parametrize("name", SCEN)
-def test_env_logic_matches_reference_fp64(golden, name):
+def test_env_logic_matches_reference_fp64(golden, name, kernel):
     """Injected physics, fp64 kernel: env logic equals the reference's golden outputs."""
     r = rec(golden, name)
-    o = run_scenario(r, "fp64", skip_physics=True)
+    o = run_scenario(r, "fp64", skip_physics=True, kernel=kernel)
     np.testing.assert_array_equal(o["done"], r["done"])
     np.testing.assert_array_equal(o["frame"], r["book_frame"].astype(np.int32))
     np.testing.assert_array_equal(o["book"][:, N.BK["cur_timestep"]], r["book_cur_timestep"])
@@ -98,11 +99,12 @@ def test_env_logic_matches_reference_fp64(golden, name):
         np.testing.assert_allclose(o["book"][:, N.BK[k]], r["book_" + k], rtol=1e-12, atol=1e-12, err_msg=k)
 
 
+@pytest.mark.parametrize("kernel", [1, 0])
 @pytest.mark.parametrize("name", SCEN)
-def test_env_logic_matches_reference_fp32(golden, name):
+def test_env_logic_matches_reference_fp32(golden, name, kernel):
     """Injected physics, fp32 kernel (the benchmarked build): FK in fp32."""
     r = rec(golden, name)
-    o = run_scenario(r, "fp32", skip_physics=True)
+    o = run_scenario(r, "fp32", skip_physics=True, kernel=kernel)
     np.testing.assert_array_equal(o["done"], r["done"])
     np.testing.assert_array_equal(o["frame"], r["book_frame"].astype(np.int32))
     np.testing.assert_allclose(o["obs"], r["obs"], rtol=2e-5, atol=2e-5)
@@ -110,12 +112,13 @@ def test_env_logic_matches_reference_fp32(golden, name):
     np.testing.assert_allclose(o["book"][:, N.BK["target"]:N.BK["target"] + 3], r["book_target"], atol=1e-5)
 
 
+@pytest.mark.parametrize("kernel", [1, 0])
 @pytest.mark.parametrize("name", SCEN)
-def test_physics_fp64_matches_oracle(golden, name):
+def test_physics_fp64_matches_oracle(golden, name, kernel):
     """Full step, fp64 kernel physics (world-frame ABA, merged multi-dof bodies) vs the fp64 oracle
     (local-frame ABA over pybullet's 32-link layout, H^-1 J^T responses)."""
     r = rec(golden, name)
-    o = run_scenario(r, "fp64", skip_physics=False)
+    o = run_scenario(r, "fp64", skip_physics=False, kernel=kernel)
     err = np.abs(o["phys"] - r["state_post"])
     assert err.max() < 1e-6, "max state err %.3g at %s" % (err.max(), np.unravel_index(err.argmax(), err.shape))
     np.testing.assert_array_equal(o["done"], r["done"])
@@ -123,12 +126,13 @@ def test_physics_fp64_matches_oracle(golden, name):
     np.testing.assert_allclose(o["rew"], r["reward"], rtol=1e-5, atol=1e-5)
 
 
-def test_physics_fp32_matches_oracle_statistics(golden):
+@pytest.mark.parametrize("kernel", [1, 0])
+def test_physics_fp32_matches_oracle_statistics(golden, kernel):
     """Full step, fp32 kernel physics vs fp64 oracle over every recorded step of every scenario."""
     errs, rerr, dmis, n = [], [], 0, 0
     for name in scenarios(golden):
         r = rec(golden, name)
-        o = run_scenario(r, "fp32", skip_physics=False)
+        o = run_scenario(r, "fp32", skip_physics=False, kernel=kernel)
         errs.append(np.abs(o["obs"] - r["obs"]).max(axis=1))
         rerr.append(np.abs(o["rew"] - r["reward"]))
         dmis += int((o["done"] != r["done"]).sum())
@@ -141,12 +145,13 @@ def test_physics_fp32_matches_oracle_statistics(golden):
     assert dmis <= max(1, n // 100)
 
 
+@pytest.mark.parametrize("kernel", [1, 0])
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
-def test_reset_matches_oracle(precision):
+def test_reset_matches_oracle(precision, kernel):
     """reset()/resetFromFrame with lane RNG draws: kernel vs oracle (low_level_env.py:224-305)."""
     clip = load_clip("motion08_03")
     n = 64
-    env = HumanoidVecEnv(n, clips=(clip,), seed=123, precision=precision)
+    env = HumanoidVecEnv(n, clips=(clip,), seed=123, precision=precision, kernel=kernel)
     yaw = np.linspace(-90, 90, n)
     sf = np.where(np.arange(n) % 2 == 0, -1, np.arange(n) % clip.max_frame - 5).astype(np.int32)
     sf = np.where(sf < 0, -1, np.abs(sf))
@@ -164,10 +169,11 @@ def test_reset_matches_oracle(precision):
     env.close()
 
 
-def test_rollout_properties_at_scale():
+@pytest.mark.parametrize("kernel", [1, 0])
+def test_rollout_properties_at_scale(kernel):
     """4096 lanes x 200 auto-reset steps (bench shape): finite, frames/timesteps consistent."""
     n = 4096
-    env = HumanoidVecEnv(n, clips=("motion02_04",), seed=5)
+    env = HumanoidVecEnv(n, clips=("motion02_04",), seed=5, kernel=kernel)
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(0)
     prev_t = np.zeros(n)
@@ -206,14 +212,17 @@ def test_graph_replay_equals_eager():
     e1.close(); e2.close()
 
 
-def test_nonfinite_action_flagged():
-    env = HumanoidVecEnv(4, clips=("motion09_03",))
+@pytest.mark.parametrize("kernel", [1, 0])
+def test_nonfinite_action_flagged(kernel):
+    env = HumanoidVecEnv(5, clips=("motion09_03",), kernel=kernel)
     env.reset()
-    a = torch.zeros(4, 17, device="cuda")
+    a = torch.zeros(5, 17, device="cuda")
     a[2, 5] = float("nan")
     env.step(a)
     assert env.error_flags() & N.HUM_EFLAG_NONFINITE_ACTION
     assert env.done[2].item() == 1
+    ph, _ = env.get_state()
+    assert np.isfinite(ph).all()
     env.close()
 
 

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 databases (kernel-trace/stats + FETCH_SIZE / WRITE_SIZE passes) into profiles/.
+
+usage: tools/prof_summary.py TAG [prof_root=gpurun_out] [lanes=4096] [clip=motion02_04] [precision=fp32]
+Writes profiles/<TAG>_kernel_stats.txt and updates profiles/pmc_traffic.json (bench.py reads it).
+HBM bytes per launch follow MI355X_MICROARCH.md: FETCH_SIZE counts half the bytes of wide coalesced
+streaming reads on gfx950 (reported both raw and x2); WRITE_SIZE is exact for 16-B stores.
+"""
+import json
+import os
+import sqlite3
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    root = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out")
+    lanes = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+    clip = sys.argv[4] if len(sys.argv) > 4 else "motion02_04"
+    prec = sys.argv[5] if len(sys.argv) > 5 else "fp32"
+    out = []
+    con = sqlite3.connect(os.path.join(root, "prof_kt", "run_results.db"))
+    out.append("# rocprofv3 --kernel-trace --stats -T  (bench.py, %d lanes, %s, %s)" % (lanes, clip, prec))
+    out.append("%-48s %8s %14s %12s %8s" % ("kernel", "calls", "total_ns", "avg_ns", "pct"))
+    step_avg = None
+    for r in con.execute("select name,total_calls,total_duration,average,percentage from top_kernels"):
+        out.append("%-48s %8d %14.0f %12.1f %8.3f" % r)
+        if r[0] == "step_kernel":
+            step_avg = r[3]
+    row = con.execute("select vgpr_count, accum_vgpr_count, sgpr_count, scratch_size, workgroup_x, grid_x from kernels "
+                      "where name='step_kernel' limit 1").fetchone()
+    if row:
+        out.append("step_kernel resources: vgpr=%s agpr=%s sgpr=%s scratch/lane=%s wg=%s grid=%s" % row)
+    pmc = {}
+    for db, ctr in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
+        p = os.path.join(root, db, "run_results.db")
+        if not os.path.exists(p):
+            continue
+        c = sqlite3.connect(p)
+        vals = [v for (v,) in c.execute("select value from counters_collection where kernel_name='step_kernel' and "
+                                        "counter_name=?", (ctr,))]
+        if vals:
+            pmc[ctr] = sum(vals) / len(vals) * 1024.0   # KB -> bytes per launch
+            out.append("%s step_kernel: %.1f KB/launch avg over %d launches" % (ctr, pmc[ctr] / 1024, len(vals)))
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        traffic = 2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]
+        out.append("HBM traffic per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction): %.3e B = %.1f B/env-step"
+                   % (traffic, traffic / lanes))
+        tp = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        tj = json.load(open(tp)) if os.path.exists(tp) else {}
+        tj["%s_%d_%s" % (clip, lanes, prec)] = {
+            "bytes_per_launch": traffic, "fetch_size_bytes_raw": pmc["FETCH_SIZE"], "write_size_bytes": pmc["WRITE_SIZE"],
+            "step_kernel_avg_ns": step_avg, "source": "profiles/%s_kernel_stats.txt" % tag}
+        json.dump(tj, open(tp, "w"), indent=1)
+    txt = "\n".join(out) + "\n"
+    open(os.path.join(REPO, "profiles", "%s_kernel_stats.txt" % tag), "w").write(txt)
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()
