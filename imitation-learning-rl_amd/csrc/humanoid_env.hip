@@ -322,11 +322,8 @@ __global__ void __launch_bounds__(64) step_group_kernel(KArgs a) {
     const bool valid = i < a.n;
     GroupLDS<T>& S = sh[ge];
     const ModelTab<T>& M = tab<T>();
-    for (int e = l; e < HUM_NSTATE; e += GL) {
-        T v = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
-        S.st[e] = v;
-        S.st0[e] = v;
-    }
+    for (int e = l; e < HUM_NSTATE; e += GL)
+        S.st[e] = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
     bool fin = true;
     for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60), float32 product
         const float av = valid ? a.act[(long)i * HUM_NACT + k] : 0.f;
@@ -339,8 +336,10 @@ __global__ void __launch_bounds__(64) step_group_kernel(KArgs a) {
     unsigned ef = 0;
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS)) {
 #pragma unroll 1
-        for (int s = 0; s < a.P.nsub; s++) group_substep(a.P, S, l, ef);
+        for (int s = 0; s < a.P.nsub; s++)
+            group_substep(a.P, S, (T*)a.scratch + (long)(valid ? i : 0) * GROW_PER_ENV, l, ef);
     }
+    PHASE_INIT;
     if (valid && l == 0) {
         Book b;
         load_book(a, i, b);
@@ -360,6 +359,7 @@ __global__ void __launch_bounds__(64) step_group_kernel(KArgs a) {
             post_step(a, i, st, b, act, ef);
         }
     }
+    PHASE(10);
     if (ef) atomicOr(a.eflags, ef);
 }
 
@@ -544,7 +544,8 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (st == hipSuccess) st = hipMalloc(&e->d.phys, HUM_NSTATE * n * e->real_size);
     if (st == hipSuccess) st = hipMalloc((void**)&e->d.bi, NBOOK_I * n * sizeof(int));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d.bd, NBOOK_D * n * sizeof(double));
-    if (st == hipSuccess) st = hipMalloc(&e->d.scratch, (size_t)SCRATCH_PER_LANE * n * e->real_size);
+    if (st == hipSuccess)   // per-lane rows (kernel 0) or the per-env row spill region (kernel 1)
+        st = hipMalloc(&e->d.scratch, (size_t)(cfg->kernel == 1 ? GROW_PER_ENV : SCRATCH_PER_LANE) * n * e->real_size);
     if (st == hipSuccess) st = hipMalloc((void**)&e->eflags, sizeof(unsigned));
     if (st == hipSuccess) st = hipMemset(e->d.bi, 0, NBOOK_I * n * sizeof(int));
     if (st == hipSuccess) st = hipMemset(e->d.bd, 0, NBOOK_D * n * sizeof(double));
@@ -855,6 +856,19 @@ int hum_sync(hum_env* e) {
 }
 
 int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
+
+#ifdef HUM_PHASE_TIMING
+// diagnostic builds only: accumulated s_memtime cycles per cooperative-kernel phase (thread 0 of each block)
+int hum_debug_phase_cycles(unsigned long long* out16, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase_cycles), 16 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
+    }
+    return HUM_OK;
+}
+#endif
 void* hum_stream(hum_env* e) { return e ? (void*)e->stream : nullptr; }
 
 }  // extern "C"

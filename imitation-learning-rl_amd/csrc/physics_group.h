@@ -83,30 +83,45 @@ template <typename T> __device__ inline const ModelTab<T>& tab();
 template <> __device__ inline const ModelTab<float>& tab<float>() { return kTabF; }
 template <> __device__ inline const ModelTab<double>& tab<double>() { return kTabD; }
 
+constexpr int MAXR_LDS = 30;                 // rows kept in LDS; rows beyond spill to a per-env global region
+constexpr int GROW_PER_ENV = (MAXR_G - MAXR_LDS) * RW;
+
 template <typename T>
-struct GroupLDS {
+struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront per SIMD
     T st[HUM_NSTATE + 1];
-    T st0[HUM_NSTATE + 1];      // pre-step state (restored for lanes with a non-finite action)
     T tau[NDOF + 3];
     T nu[NV + 1];
-    T acc[NV + 1];
     T R[NB][9], o[NB][3], u[NDOF][3];
-    T U[NDOF][6], Dinv[NB][9], L0[21], uu[NDOF];
-    T c[NB][6];
+    T U[NDOF][6], Dinv[NB][9], L0[21];
     union {
-        struct {
-            T V[NB][6], IA[NB][21], pA[NB][6];
-            T W[3][6], D[9], pa[6];
+        struct {   // articulated-body pass (dead once the accelerations are known)
+            T V[NB][6], c[NB][6], IA[NB][21], pA[NB][6], uu[NDOF + 1];
         } aba;
-        struct {
+        struct {   // contacts + constraint rows
             T gp[NGEOM][2][3];
             T con[MAXC_G][12];
-            T row[MAXR_G][RW];
+            T row[MAXR_LDS][RW];
             int rdesc[MAXR_G];   // limit rows: dof | side << 8
         } cr;
     } x;
-    int nl, nc, flag;
 };
+
+// ---- diagnostic phase timing (compiled only with -DHUM_PHASE_TIMING; never in the shipped library)
+#ifdef HUM_PHASE_TIMING
+__device__ unsigned long long g_phase_cycles[16];
+#define PHASE(k)                                                                 \
+    do {                                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
+            atomicAdd(&g_phase_cycles[k], t_ - t_last_);                         \
+            t_last_ = t_;                                                        \
+        }                                                                        \
+    } while (0)
+#define PHASE_INIT unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
+#else
+#define PHASE(k) do { } while (0)
+#define PHASE_INIT do { } while (0)
+#endif
 
 __device__ inline void wave_sync() {   // cross-lane LDS ordering inside one wavefront
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -263,9 +278,10 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
 // ------------------------------------------------------------------------- one cooperative substep
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
 template <typename T>
-__device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, unsigned& ef) {
+__device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, T* grow, const int l, unsigned& ef) {
     const ModelTab<T>& M = tab<T>();
     const T dt = (T)P.dt;
+    PHASE_INIT;
     // ---- FK (every lane, registers); lane 0 publishes
     {
         T st[HUM_NSTATE];
@@ -292,6 +308,7 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
         }
     }
     __syncthreads();
+    PHASE(1);
     // ---- ABA pass 1: lane b = body b
     if (l < NB) {
         const int b = l;
@@ -385,99 +402,105 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
             for (int i = 0; i < 3; i++) { pA[i] -= n[i] + cxF[i]; pA[3 + i] -= F[i]; }
         }
 #pragma unroll
-        for (int e = 0; e < 6; e++) { S.x.aba.V[b][e] = V[e]; S.c[b][e] = cb[e]; S.x.aba.pA[b][e] = pA[e]; }
+        for (int e = 0; e < 6; e++) { S.x.aba.V[b][e] = V[e]; S.x.aba.c[b][e] = cb[e]; S.x.aba.pA[b][e] = pA[e]; }
 #pragma unroll
         for (int q = 0; q < 21; q++) S.x.aba.IA[b][q] = IA[q];
     }
     __syncthreads();
-    // ---- ABA pass 2: body by body, matrix entries split over the 16 lanes
+    PHASE(2);
+    // ---- ABA pass 2 (leaves -> root): every lane computes the body update redundantly in registers
+    //      (no barriers); lane q publishes entry q of IA_parent / pA_parent, lane 0 the factorisation.
     auto& A = S.x.aba;
 #pragma unroll
     for (int b = NB - 1; b >= 1; b--) {
         const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
-        // U = IA S (6k entries) ; u = tau - S^T pA (k entries, lanes 16-k..15 reuse)
-        for (int q = l; q < 6 * k; q += GL) {
-            const int j = q / 6, r = q % 6, d = d0 + j;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[b], S.u[d], Sc + 3);
-            T s = 0;
+        T IA[21], pAb[6], cb[6], Sc[3][6], U[3][6], D[9], Di[9], uj[3], W[3][6];
 #pragma unroll
-            for (int f = 0; f < 6; f++) s += A.IA[b][sidx(r, f)] * Sc[f];
-            S.U[d][r] = s;
-        }
-        if (l < k) {
-            const int j = l, d = d0 + j;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[b], S.u[d], Sc + 3);
+        for (int q = 0; q < 21; q++) IA[q] = A.IA[b][q];
+#pragma unroll
+        for (int e = 0; e < 6; e++) { pAb[e] = A.pA[b][e]; cb[e] = A.c[b][e]; }
+#pragma unroll
+        for (int j = 0; j < k; j++) {
+            const int d = d0 + j;
+            Sc[j][0] = S.u[d][0]; Sc[j][1] = S.u[d][1]; Sc[j][2] = S.u[d][2];
+            cross3(S.o[b], S.u[d], Sc[j] + 3);
+            symmv(IA, Sc[j], U[j]);
             T sp = 0;
 #pragma unroll
-            for (int e = 0; e < 6; e++) sp += Sc[e] * A.pA[b][e];
-            T uj = S.tau[d] - sp;
-            if (P.joint_damping) uj -= M.damp[d] * S.nu[6 + d];
-            S.uu[d] = uj;
+            for (int e = 0; e < 6; e++) sp += Sc[j][e] * pAb[e];
+            uj[j] = S.tau[d] - sp;
+            if (P.joint_damping) uj[j] -= M.damp[d] * S.nu[6 + d];
         }
-        __syncthreads();
-        // D = S^T U (+ dt*damping), inverse by lane 0
-        if (l == 0) {
-            T D[9], Di[9];
 #pragma unroll
-            for (int i = 0; i < k; i++) {
-                const int d = d0 + i;
-                T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-                cross3(S.o[b], S.u[d], Sc + 3);
+        for (int i = 0; i < k; i++) {
 #pragma unroll
-                for (int j = 0; j < k; j++) {
-                    T s = 0;
+            for (int j = 0; j < k; j++) {
+                T t = 0;
 #pragma unroll
-                    for (int e = 0; e < 6; e++) s += Sc[e] * S.U[d0 + j][e];
-                    D[3 * i + j] = s;
-                }
-                if (P.joint_damping) D[4 * i] += dt * M.damp[d];
+                for (int e = 0; e < 6; e++) t += Sc[i][e] * U[j][e];
+                D[3 * i + j] = t;
             }
-            if (k == 1) small_inverse<T, 1>(D, Di);
-            else if (k == 2) small_inverse<T, 2>(D, Di);
-            else small_inverse<T, 3>(D, Di);
+            if (P.joint_damping) D[4 * i] += dt * M.damp[d0 + i];
+        }
+        if (k == 1) small_inverse<T, 1>(D, Di);
+        else if (k == 2) small_inverse<T, 2>(D, Di);
+        else small_inverse<T, 3>(D, Di);
+#pragma unroll
+        for (int j = 0; j < k; j++)
+#pragma unroll
+            for (int e = 0; e < 6; e++) {
+                T t = 0;
+#pragma unroll
+                for (int i = 0; i < k; i++) t += U[i][e] * Di[3 * i + j];
+                W[j][e] = t;
+            }
+        // Ia = IA - W U^T (in place), pa = pA + Ia c + W u
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int cc = r; cc < 6; cc++) {
+                T t = IA[sidx(r, cc)];
+#pragma unroll
+                for (int j = 0; j < k; j++) t -= W[j][r] * U[j][cc];
+                IA[sidx(r, cc)] = t;
+            }
+        T pa[6];
+        symmv(IA, cb, pa);
+#pragma unroll
+        for (int e = 0; e < 6; e++) {
+            T t = pAb[e] + pa[e];
+#pragma unroll
+            for (int j = 0; j < k; j++) t += W[j][e] * uj[j];
+            pa[e] = t;
+        }
+        // publish: lane q -> IA_p[q] (and q+16), lanes 0..5 -> pA_p, lane 0 -> U, Dinv, uu
+        T v0 = 0, v1 = 0, v2 = 0;
+#pragma unroll
+        for (int q = 0; q < 21; q++) {
+            if (q == l) v0 = IA[q];
+            if (q == l + GL) v1 = IA[q];
+        }
+#pragma unroll
+        for (int e = 0; e < 6; e++)
+            if (e == l) v2 = pa[e];
+        A.IA[p][l] += v0;
+        if (l + GL < 21) A.IA[p][l + GL] += v1;
+        if (l < 6) A.pA[p][l] += v2;
+        if (l == 0) {
+#pragma unroll
+            for (int j = 0; j < k; j++) {
+#pragma unroll
+                for (int e = 0; e < 6; e++) S.U[d0 + j][e] = U[j][e];
+                A.uu[d0 + j] = uj[j];
+            }
 #pragma unroll
             for (int q = 0; q < 9; q++) S.Dinv[b][q] = Di[q];
         }
-        __syncthreads();
-        // W = U Dinv
-        for (int q = l; q < 6 * k; q += GL) {
-            const int j = q / 6, r = q % 6;
-            T s = 0;
-#pragma unroll
-            for (int i = 0; i < k; i++) s += S.U[d0 + i][r] * S.Dinv[b][3 * i + j];
-            A.W[j][r] = s;
-        }
-        __syncthreads();
-        // Ia = IA - W U^T (21 entries) ; IA_p += Ia
-#pragma unroll
-        for (int q0 = 0; q0 < 21; q0 += GL) {
-            const int q = q0 + l;
-            if (q < 21) {
-                int r = 0, cc = q;   // packed upper index -> (r, c)
-                while (cc >= 6 - r) { cc -= 6 - r; r++; }
-                cc += r;
-                T s = A.IA[b][q];
-#pragma unroll
-                for (int j = 0; j < k; j++) s -= A.W[j][r] * S.U[d0 + j][cc];
-                A.IA[b][q] = s;
-                A.IA[p][q] += s;
-            }
-        }
-        __syncthreads();
-        // pa = pA + Ia c + W u ; pA_p += pa
-        if (l < 6) {
-            T s = A.pA[b][l];
-#pragma unroll
-            for (int f = 0; f < 6; f++) s += A.IA[b][sidx(l, f)] * S.c[b][f];
-#pragma unroll
-            for (int j = 0; j < k; j++) s += A.W[j][l] * S.uu[d0 + j];
-            A.pA[p][l] += s;
-        }
-        __syncthreads();
+        wave_sync();
     }
-    // ---- base + pass 3 (redundant on every lane; lane 0 publishes)
+    __syncthreads();
+    PHASE(3);
+    // ---- base + pass 3 (redundant on every lane); lane 0 publishes L0 and nu* = clamp(nu + dt acc)
     {
         T L[21], a[NB][6];
         T IA0[21];
@@ -493,51 +516,47 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
             const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
             T ap[6], r[3];
 #pragma unroll
-            for (int e = 0; e < 6; e++) ap[e] = a[p][e] + S.c[b][e];
+            for (int e = 0; e < 6; e++) ap[e] = a[p][e] + A.c[b][e];
 #pragma unroll
             for (int j = 0; j < k; j++) {
-                T s = S.uu[d0 + j];
+                T t = A.uu[d0 + j];
 #pragma unroll
-                for (int e = 0; e < 6; e++) s -= S.U[d0 + j][e] * ap[e];
-                r[j] = s;
+                for (int e = 0; e < 6; e++) t -= S.U[d0 + j][e] * ap[e];
+                r[j] = t;
             }
 #pragma unroll
             for (int e = 0; e < 6; e++) a[b][e] = ap[e];
 #pragma unroll
             for (int i = 0; i < k; i++) {
-                T s = 0;
+                T t = 0;
 #pragma unroll
-                for (int j = 0; j < k; j++) s += S.Dinv[b][3 * i + j] * r[j];
-                acc[6 + d0 + i] = s;
+                for (int j = 0; j < k; j++) t += S.Dinv[b][3 * i + j] * r[j];
+                acc[6 + d0 + i] = t;
                 const int d = d0 + i;
                 T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
                 cross3(S.o[b], S.u[d], Sc + 3);
 #pragma unroll
-                for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * s;
+                for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * t;
             }
         }
-        T nu0[6];
+        T nu[NV];
 #pragma unroll
-        for (int e = 0; e < 6; e++) nu0[e] = S.nu[e];
+        for (int e = 0; e < NV; e++) nu[e] = S.nu[e];
         T wxv[3];
-        cross3(nu0, nu0 + 3, wxv);
+        cross3(nu, nu + 3, wxv);
 #pragma unroll
         for (int i = 0; i < 3; i++) { acc[i] = a[0][i]; acc[3 + i] = a[0][3 + i] + wxv[i]; }
-        __syncthreads();   // everyone has read A.IA/pA (the union is reused below)
+        __syncthreads();   // every lane has read the ABA union and nu
         if (l == 0) {
+            const T vmax = (T)P.max_coord_vel;
 #pragma unroll
             for (int q = 0; q < 21; q++) S.L0[q] = L[q];
 #pragma unroll
-            for (int e = 0; e < NV; e++) S.acc[e] = acc[e];
+            for (int e = 0; e < NV; e++) S.nu[e] = clampT(nu[e] + dt * acc[e], -vmax, vmax);
         }
     }
     __syncthreads();
-    // ---- nu* = clamp(nu + dt acc)
-    {
-        const T vmax = (T)P.max_coord_vel;
-        S.nu[l] = clampT(S.nu[l] + dt * S.acc[l], -vmax, vmax);
-        if (l < NV - GL) S.nu[GL + l] = clampT(S.nu[GL + l] + dt * S.acc[GL + l], -vmax, vmax);
-    }
+    PHASE(4);
     // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
     auto& C = S.x.cr;
     for (int g = l; g < NGEOM; g += GL) {
@@ -571,6 +590,7 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
         nl += __popcll(gm1) + __popcll(gm2);
     }
     __syncthreads();
+    PHASE(5);
     // ---- contacts: candidate c = 16*round + lane, compacted in candidate order
     const int maxc = P.max_contacts < MAXC_G ? P.max_contacts : MAXC_G;
     int nc = 0, over = 0;
@@ -630,13 +650,14 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
     if (nc > maxc) { nc = maxc; over = 1; }
     if (over) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
     __syncthreads();
+    PHASE(6);
     // ---- rows: one per lane (limits, normals, frictions), Jacobian + response
     const int nrows = nl + 3 * nc;
     for (int r = l; r < nrows; r += GL) {
         T J[NV], Mi[NV];
 #pragma unroll
         for (int e = 0; e < NV; e++) J[e] = 0;
-        T* R = C.row[r];
+        T* R = r < MAXR_LDS ? C.row[r] : grow + (r - MAXR_LDS) * RW;
         if (r < nl) {
             const int d = C.rdesc[r] & 0xff, side = C.rdesc[r] >> 8;
             const T sg = side == 0 ? T(1) : T(-1);
@@ -710,32 +731,36 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
         }
     }
     __syncthreads();
-    // ---- PGS (lane l owns nu[l] and nu[16+l])
+    PHASE(7);
+    // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
+    //      re-reads values it wrote itself, so no cross-lane LDS ordering is needed inside the loop.
     T n0 = S.nu[l], n1 = l < NV - GL ? S.nu[GL + l] : T(0);
-    for (int it = 0; it < P.iters; it++) {
-        for (int r = 0; r < nrows; r++) {
-            T* R = C.row[r];
-            if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
-                const T ln = C.row[nl + ((r - nl - nc) >> 1)][2 * NV + 3];
-                const T mu = R[2 * NV + 5];
-                R[2 * NV + 1] = -mu * ln;
-                R[2 * NV + 2] = mu * ln;
-            }
-            T part = R[l] * n0 + (l < NV - GL ? R[GL + l] * n1 : T(0));
-            const T jv = row_sum(part);
-            const T lam = R[2 * NV + 3];
-            const T lnew = clampT(lam + R[2 * NV + 4] * (R[2 * NV + 0] - jv), R[2 * NV + 1], R[2 * NV + 2]);
-            const T dl = lnew - lam;
-            wave_sync();
-            R[2 * NV + 3] = lnew;
-            n0 += R[NV + l] * dl;
-            if (l < NV - GL) n1 += R[NV + GL + l] * dl;
-            wave_sync();
+    auto lam_of = [&](int r) -> T { return r < MAXR_LDS ? C.row[r][2 * NV + 3] : grow[(r - MAXR_LDS) * RW + 2 * NV + 3]; };
+    auto solve = [&](T* R, int r) {
+        T lo = R[2 * NV + 1], hi = R[2 * NV + 2];
+        if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
+            const T mu = R[2 * NV + 5];
+            const T ln = lam_of(nl + ((r - nl - nc) >> 1));
+            lo = -mu * ln;
+            hi = mu * ln;
         }
+        const T part = R[l] * n0 + (l < NV - GL ? R[GL + l] * n1 : T(0));
+        const T m0 = R[NV + l], m1 = l < NV - GL ? R[NV + GL + l] : T(0);
+        const T jv = row_sum(part);
+        const T lam = R[2 * NV + 3];
+        const T lnew = clampT(lam + R[2 * NV + 4] * (R[2 * NV + 0] - jv), lo, hi);
+        const T dl = lnew - lam;
+        R[2 * NV + 3] = lnew;
+        n0 += m0 * dl;
+        n1 += m1 * dl;
+    };
+    for (int it = 0; it < P.iters; it++) {
+        const int nr_lds = nrows < MAXR_LDS ? nrows : MAXR_LDS;
+        for (int r = 0; r < nr_lds; r++) solve(C.row[r], r);
+        for (int r = MAXR_LDS; r < nrows; r++) solve(grow + (r - MAXR_LDS) * RW, r);
     }
     S.nu[l] = n0;
     if (l < NV - GL) S.nu[GL + l] = n1;
-    __syncthreads();
     // ---- integrate (lanes split the state), lane 0 the quaternion
     {
         if (l < 3) { S.st[10 + l] = S.nu[l]; S.st[7 + l] = S.nu[3 + l]; S.st[l] += dt * S.nu[3 + l]; }
@@ -766,6 +791,7 @@ __device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, const int l, 
         }
     }
     __syncthreads();
+    PHASE(9);
 }
 
 }  // namespace hk

@@ -83,6 +83,8 @@ def lib():
     L.hum_stream.restype = vp
     for name in EXPORTS:
         getattr(L, name)  # AttributeError if the library lacks a declared symbol
+    if hasattr(L, "hum_debug_phase_cycles"):   # diagnostic builds only
+        L.hum_debug_phase_cycles.argtypes = [vp, ctypes.c_int]
     _lib = L
     return L
 
