@@ -18,10 +18,10 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "imitation-learning-rl_amd"))
 
-# algorithmic HBM bytes per env-step of the step kernel (DESIGN.md "Roofline"): reads + writes the
-# kernel must do per lane: physics state 47 f32 (r+w), bookkeeping 29 f64 + 8 i32 read / 29 f64 + 8 i32
-# written, action 17 f32, obs 70 f32, reward f32, done u8, frame i32.
-BYTES_PER_STEP_FP32 = 2 * 47 * 4 + 2 * (29 * 8 + 8 * 4) + 17 * 4 + 70 * 4 + 4 + 1 + 4
+# algorithmic HBM bytes per env-step of the step kernel (DESIGN.md "Roofline"): what the kernel must read
+# and write per env: physics state 47 x f32 (read + write), bookkeeping 23 x f64 + 8 x i32 (read + write),
+# action 17 x f32, obs 70 x f32, reward f32, done u8, frame i32  = 1165 B (clip tables are cache resident).
+BYTES_PER_STEP_FP32 = 2 * 47 * 4 + 2 * (23 * 8 + 8 * 4) + 17 * 4 + 70 * 4 + 4 + 1 + 4
 HBM_PEAK_GBS = 8000.0
 
 
