@@ -134,7 +134,7 @@ def main():
             except Exception:
                 traffic = None
         out = {
-            "metric": "env steps/sec at N parallel humanoids (4096 per MI355X), motion02_04 low-level imitation",
+            "metric": "env steps/sec at N parallel humanoids, 1/2/4/8 MI355X; obs/reward max-abs-err vs PyBullet",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": wall_max / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
@@ -146,6 +146,9 @@ def main():
                          "bytes_per_env_step": bpl, "kernel_ms": kern_ms},
             "error_flags": flags,
         }
+        pp = os.path.join(REPO, "profiles", "parity_fp32_kernel1.json")   # written by tests/test_gpu_parity.py
+        if a.precision == "fp32" and os.path.exists(pp):
+            out["parity"] = dict(json.load(open(pp)), source="profiles/parity_fp32_kernel1.json")
         if world == 1 and a.cpu_seconds > 0:
             workers = a.cpu_workers or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, workers)

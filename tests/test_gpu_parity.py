@@ -11,6 +11,9 @@ bookkeeping the reference held before step t, and the recorded action.
 Tolerances (stated per quantity below): done / frame / timestep / target decisions bit-exact;
 fp64 kernel: obs within 1 float32 ulp, reward 1e-9; fp32 kernel: obs 2e-5, reward 1e-4 (fp32 FK).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -140,6 +143,14 @@ def test_physics_fp32_matches_oracle_statistics(golden, kernel):
     errs, rerr = np.concatenate(errs), np.concatenate(rerr)
     print("fp32 physics: steps=%d obs err p50=%.2e p99=%.2e max=%.2e; reward err p50=%.2e p99=%.2e; done mismatches=%d"
           % (n, np.median(errs), np.percentile(errs, 99), errs.max(), np.median(rerr), np.percentile(rerr, 99), dmis))
+    out = os.environ.get("ILRL_PARITY_OUT")    # summary for bench.py's "parity" object (copied into profiles/)
+    if out:
+        os.makedirs(out, exist_ok=True)
+        json.dump({"vs": "fp64 CPU oracle (PyBullet absent: parity vs PyBullet unpinned)", "kernel": kernel,
+                   "precision": "fp32", "steps": n, "obs_max_abs_err": float(errs.max()),
+                   "obs_p50_abs_err": float(np.median(errs)), "obs_p99_abs_err": float(np.percentile(errs, 99)),
+                   "reward_max_abs_err": float(rerr.max()), "reward_p99_abs_err": float(np.percentile(rerr, 99)),
+                   "done_mismatches": dmis}, open(os.path.join(out, "parity_fp32_kernel%d.json" % kernel), "w"), indent=1)
     assert np.median(errs) < 1e-3
     assert np.percentile(rerr, 90) < 1e-2
     assert dmis <= max(1, n // 100)

@@ -23,27 +23,30 @@ def main():
     out = []
     con = sqlite3.connect(os.path.join(root, "prof_kt", "run_results.db"))
     out.append("# rocprofv3 --kernel-trace --stats -T  (bench.py, %d lanes, %s, %s)" % (lanes, clip, prec))
-    out.append("%-48s %8s %14s %12s %8s" % ("kernel", "calls", "total_ns", "avg_ns", "pct"))
-    step_avg = None
-    for r in con.execute("select name,total_calls,total_duration,average,percentage from top_kernels"):
-        out.append("%-48s %8d %14.0f %12.1f %8.3f" % r)
-        if r[0] == "step_kernel":
-            step_avg = r[3]
-    row = con.execute("select vgpr_count, accum_vgpr_count, sgpr_count, scratch_size, workgroup_x, grid_x from kernels "
-                      "where name='step_kernel' limit 1").fetchone()
+    # rocpd's top_kernels view reports durations in microseconds
+    out.append("%-48s %8s %14s %12s %8s" % ("kernel", "calls", "total_us", "avg_us", "pct"))
+    step_avg, kname = None, None
+    for r in con.execute("select name,total_calls,total_duration,average,percentage from top_kernels "
+                         "order by total_duration desc"):
+        out.append("%-48s %8d %14.1f %12.3f %8.3f" % r)
+        if kname is None and r[0].startswith("step"):
+            kname, step_avg = r[0], r[3]
+    kname = kname or "step_group_kernel"
+    row = con.execute("select vgpr_count, accum_vgpr_count, sgpr_count, scratch_size, lds_size, workgroup_x, grid_x "
+                      "from kernels where name=? limit 1", (kname,)).fetchone()
     if row:
-        out.append("step_kernel resources: vgpr=%s agpr=%s sgpr=%s scratch/lane=%s wg=%s grid=%s" % row)
+        out.append("%s resources: vgpr=%s agpr=%s sgpr=%s scratch/lane=%s lds=%s wg=%s grid=%s" % ((kname,) + row))
     pmc = {}
     for db, ctr in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
         p = os.path.join(root, db, "run_results.db")
         if not os.path.exists(p):
             continue
         c = sqlite3.connect(p)
-        vals = [v for (v,) in c.execute("select value from counters_collection where kernel_name='step_kernel' and "
-                                        "counter_name=?", (ctr,))]
+        vals = [v for (v,) in c.execute("select value from counters_collection where kernel_name=? and "
+                                        "counter_name=?", (kname, ctr))]
         if vals:
             pmc[ctr] = sum(vals) / len(vals) * 1024.0   # KB -> bytes per launch
-            out.append("%s step_kernel: %.1f KB/launch avg over %d launches" % (ctr, pmc[ctr] / 1024, len(vals)))
+            out.append("%s %s: %.1f KB/launch avg over %d launches" % (ctr, kname, pmc[ctr] / 1024, len(vals)))
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         traffic = 2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]
         out.append("HBM traffic per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction): %.3e B = %.1f B/env-step"
@@ -52,7 +55,7 @@ def main():
         tj = json.load(open(tp)) if os.path.exists(tp) else {}
         tj["%s_%d_%s" % (clip, lanes, prec)] = {
             "bytes_per_launch": traffic, "fetch_size_bytes_raw": pmc["FETCH_SIZE"], "write_size_bytes": pmc["WRITE_SIZE"],
-            "step_kernel_avg_ns": step_avg, "source": "profiles/%s_kernel_stats.txt" % tag}
+            "kernel": kname, "kernel_avg_us": step_avg, "source": "profiles/%s_kernel_stats.txt" % tag}
         json.dump(tj, open(tp, "w"), indent=1)
     txt = "\n".join(out) + "\n"
     open(os.path.join(REPO, "profiles", "%s_kernel_stats.txt" % tag), "w").write(txt)
