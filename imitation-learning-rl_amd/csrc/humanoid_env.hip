@@ -47,7 +47,7 @@ struct KArgs {
     unsigned long long seed;
     long long lane_offset;
     PhysParams P;
-    ClipDev clips[HUM_MAX_CLIPS];
+    const ClipDev* clips;   // device array [HUM_MAX_CLIPS] (a by-value array here is dynamically indexed -> scratch copy)
     const double* pred;
     int npred;
     void* phys;
@@ -313,12 +313,14 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
     post_step(a, i, st, b, act, ef);
 }
 
-// Cooperative step: 16 lanes per env, 4 envs per 64-thread block (one wavefront), env working set in LDS.
-template <typename T>
-__global__ void __launch_bounds__(64) step_group_kernel(KArgs a) {
-    __shared__ GroupLDS<T> sh[EPB];
+// Cooperative step: 16 lanes per env, EPB_ envs per block of EPB_*16 threads (one wavefront), env working
+// set in LDS.  EPB_ = 4 fills the wave; EPB_ = 2 leaves half of it idle but lets a SIMD hold two waves
+// (19.3 KB LDS per block), so one wave's LDS/memory waits overlap the other's VALU issue.
+template <typename T, int EPB_>
+__global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
+    __shared__ GroupLDS<T> sh[EPB_];
     const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
-    const int i = blockIdx.x * EPB + ge;
+    const int i = blockIdx.x * EPB_ + ge;
     const bool valid = i < a.n;
     GroupLDS<T>& S = sh[ge];
     const ModelTab<T>& M = tab<T>();
@@ -439,6 +441,7 @@ struct hum_env {
     size_t real_size;
     double* clip_dev[HUM_MAX_CLIPS];
     ClipDev clips[HUM_MAX_CLIPS];
+    ClipDev* clips_dev;   // device copy of clips[] read by the kernels
     bool clip_set[HUM_MAX_CLIPS];
     double* pred;
     int npred;
@@ -473,7 +476,7 @@ KArgs make_args(hum_env* e) {
     a.P.max_contacts = c.max_contacts;
     a.P.self_collision = c.self_collision;
     a.P.joint_damping = c.joint_damping;
-    for (int k = 0; k < HUM_MAX_CLIPS; k++) a.clips[k] = e->clips[k];
+    a.clips = e->clips_dev;
     a.pred = e->pred;
     a.npred = e->npred;
     a.phys = e->d.phys;
@@ -522,6 +525,7 @@ void hum_default_config(hum_config* c) {
     c->self_collision = 1;
     c->joint_damping = 1;
     c->kernel = 1;
+    c->envs_per_block = 4;
 }
 
 int hum_create(const hum_config* cfg, hum_env** out) {
@@ -532,6 +536,8 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (cfg->precision != 0 && cfg->precision != 1) return fail(HUM_ERR_ARG, "hum_create: precision must be 0 or 1");
     if (cfg->substeps <= 0 || cfg->solver_iters < 0) return fail(HUM_ERR_ARG, "hum_create: bad solver settings");
     if (cfg->kernel != 0 && cfg->kernel != 1) return fail(HUM_ERR_ARG, "hum_create: kernel must be 0 (per-lane) or 1 (cooperative)");
+    if (cfg->envs_per_block != 1 && cfg->envs_per_block != 2 && cfg->envs_per_block != 4)
+        return fail(HUM_ERR_ARG, "hum_create: envs_per_block must be 1, 2 or 4");
     if (cfg->max_contacts < 0 || cfg->max_contacts > (cfg->kernel == 1 ? MAXC_G : MAXC))
         return fail(HUM_ERR_ARG, "hum_create: max_contacts out of range for the selected kernel");
     HIPCHK(hipSetDevice(cfg->device));
@@ -547,6 +553,8 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (st == hipSuccess)   // per-lane rows (kernel 0) or the per-env row spill region (kernel 1)
         st = hipMalloc(&e->d.scratch, (size_t)(cfg->kernel == 1 ? GROW_PER_ENV : SCRATCH_PER_LANE) * n * e->real_size);
     if (st == hipSuccess) st = hipMalloc((void**)&e->eflags, sizeof(unsigned));
+    if (st == hipSuccess) st = hipMalloc((void**)&e->clips_dev, HUM_MAX_CLIPS * sizeof(ClipDev));
+    if (st == hipSuccess) st = hipMemset(e->clips_dev, 0, HUM_MAX_CLIPS * sizeof(ClipDev));
     if (st == hipSuccess) st = hipMemset(e->d.bi, 0, NBOOK_I * n * sizeof(int));
     if (st == hipSuccess) st = hipMemset(e->d.bd, 0, NBOOK_D * n * sizeof(double));
     if (st == hipSuccess) st = hipMemset(e->d.phys, 0, HUM_NSTATE * n * e->real_size);
@@ -576,6 +584,7 @@ int hum_destroy(hum_env* e) {
     (void)hipFree(e->d.bd);
     (void)hipFree(e->d.scratch);
     (void)hipFree(e->eflags);
+    (void)hipFree(e->clips_dev);
     (void)hipFree(e->pred);
     for (int k = 0; k < HUM_MAX_CLIPS; k++) (void)hipFree(e->clip_dev[k]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -599,6 +608,7 @@ int hum_set_clip(hum_env* e, int32_t id, const double* pos, int32_t n_pos, const
     e->clip_dev[id] = buf;
     e->clips[id] = ClipDev{buf, buf + np, buf + np + nv, buf + np + nv + nr, n_pos, n_vel, n_rel, n_ep, n_pos - 1};
     e->clip_set[id] = true;
+    HIPCHK(hipMemcpy(e->clips_dev + id, &e->clips[id], sizeof(ClipDev), hipMemcpyHostToDevice));
     return HUM_OK;
 }
 
@@ -664,9 +674,17 @@ int hum_step(hum_env* e, const float* actions, float* obs, float* reward, uint8_
     a.obs_reset = obs_reset;
     hipStream_t s = stream_of(e, stream);
     if (e->cfg.kernel == 1) {
-        const dim3 g((e->n + EPB - 1) / EPB), blk(EPB * GL);
-        if (e->cfg.precision) hipLaunchKernelGGL(step_group_kernel<double>, g, blk, 0, s, a);
-        else hipLaunchKernelGGL(step_group_kernel<float>, g, blk, 0, s, a);
+        const int epb = e->cfg.envs_per_block;
+        const dim3 g((e->n + epb - 1) / epb), blk(epb * GL);
+        if (e->cfg.precision) {
+            if (epb == 4) hipLaunchKernelGGL((step_group_kernel<double, 4>), g, blk, 0, s, a);
+            else if (epb == 2) hipLaunchKernelGGL((step_group_kernel<double, 2>), g, blk, 0, s, a);
+            else hipLaunchKernelGGL((step_group_kernel<double, 1>), g, blk, 0, s, a);
+        } else {
+            if (epb == 4) hipLaunchKernelGGL((step_group_kernel<float, 4>), g, blk, 0, s, a);
+            else if (epb == 2) hipLaunchKernelGGL((step_group_kernel<float, 2>), g, blk, 0, s, a);
+            else hipLaunchKernelGGL((step_group_kernel<float, 1>), g, blk, 0, s, a);
+        }
     } else {
         if (e->cfg.precision) hipLaunchKernelGGL(step_kernel<double>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
         else hipLaunchKernelGGL(step_kernel<float>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
@@ -682,7 +700,7 @@ int hum_step_graph(hum_env* e, const float* actions, float* obs, float* reward, 
     const void* key[6] = {actions, obs, reward, done, frame, obs_reset};
     bool same = e->graph && e->graph_k == k && e->graph_flags == flags && memcmp(key, e->graph_key, sizeof key) == 0;
     if (!same) {
-        if (e->graph) { hipGraphExecDestroy(e->graph); e->graph = nullptr; }
+        if (e->graph) { (void)hipGraphExecDestroy(e->graph); e->graph = nullptr; }
         hipGraph_t g;
         HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
         for (int t = 0; t < k; t++) {

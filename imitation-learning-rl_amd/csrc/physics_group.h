@@ -19,7 +19,6 @@
 namespace hk {
 
 constexpr int GL = 16;                       // lanes per env
-constexpr int EPB = 4;                       // envs per 64-thread block (one wavefront)
 constexpr int MAXC_G = 16;                   // contact cap of the cooperative kernel
 constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // 65 rows
 constexpr int RW = 2 * NV + 6;               // J[NV], M[NV], b, lo, hi, lam, meff, mu
@@ -278,7 +277,7 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
 // ------------------------------------------------------------------------- one cooperative substep
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
 template <typename T>
-__device__ void group_substep(const PhysParams& P, GroupLDS<T>& S, T* grow, const int l, unsigned& ef) {
+__device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>& S, T* grow, const int l, unsigned& ef) {
     const ModelTab<T>& M = tab<T>();
     const T dt = (T)P.dt;
     PHASE_INIT;

@@ -8,6 +8,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
+HUM_ABI_VERSION = 2   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 32, 12
 HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS = 1, 2
 HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
@@ -37,7 +38,8 @@ class HumConfig(ctypes.Structure):
                 ("lin_damp", ctypes.c_double), ("ang_damp", ctypes.c_double),
                 ("limit_max_impulse", ctypes.c_double), ("max_coord_vel", ctypes.c_double),
                 ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
-                ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32)]
+                ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32),
+                ("envs_per_block", ctypes.c_int32)]
 
 
 class NativeError(RuntimeError):
@@ -83,6 +85,9 @@ def lib():
     L.hum_stream.restype = vp
     for name in EXPORTS:
         getattr(L, name)  # AttributeError if the library lacks a declared symbol
+    if L.hum_abi_version() != HUM_ABI_VERSION:
+        raise NativeError("libhumenv.so ABI %d != binding ABI %d: rebuild the library"
+                          % (L.hum_abi_version(), HUM_ABI_VERSION))
     if hasattr(L, "hum_debug_phase_cycles"):   # diagnostic builds only
         L.hum_debug_phase_cycles.argtypes = [vp, ctypes.c_int]
     _lib = L

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 1
+#define HUM_ABI_VERSION 2
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -100,6 +100,9 @@ typedef struct hum_config {
     int32_t self_collision;   /* 1 */
     int32_t joint_damping;    /* 1 = implicit MJCF joint damping */
     int32_t kernel;           /* 1 = cooperative (16 lanes/env, LDS-resident; default), 0 = one env per lane */
+    int32_t envs_per_block;   /* cooperative kernel: envs per wavefront-block (4 = 64 threads (default), 2 = 32,
+                                 1 = 16).  Fewer envs per wave buys SIMD co-residency but multiplies the wave
+                                 instruction stream per env: measured 0.39 / 0.64 / 0.98 ms at 4096 envs */
 } hum_config;
 
 /* Version / build info. */

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
     for name in decl:
         assert hasattr(L, name), name
     assert set(decl) == set(N.EXPORTS)
-    assert L.hum_abi_version() == 1
+    assert L.hum_abi_version() == N.HUM_ABI_VERSION
 
 
 def test_config_layout_matches_header(tmp_path):
