@@ -31,12 +31,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--lanes", type=int, default=4096, help="env lanes per GPU")
-    ap.add_argument("--clip", default="motion02_04")
+    ap.add_argument("--clip", default="motion02_04", help="clip name, or 'all' = the four CMU clips round-robin per "
+                                                          "lane (BASELINE config 3)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--block", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0 = min(16, cpus))")
     ap.add_argument("--phys", action="append", default=[], help="physics override k=v (hum_config field), diagnostics")
+    ap.add_argument("--hier", action="store_true",
+                    help="config 5: HierarchicalHumanoidEnv two-level rollout (hum_hier_step), clip motion09_03")
     return ap.parse_args()
 
 
@@ -90,13 +93,24 @@ def main():
     for kv in a.phys:
         k, v = kv.split("=")
         phys[k] = float(v) if "." in v else int(v)
-    env = HumanoidVecEnv(n, clips=(a.clip,), seed=0, device=local, lane_offset=rank * n, precision=a.precision,
-                         block_size=a.block, **phys)
-    env.reset()
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [(torch.rand(n, 17, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
+    if a.hier:
+        from ilrl_amd.hier_env import HIER_CLIP, HierVecEnv
+        a.clip = HIER_CLIP
+        env = HierVecEnv(n, seed=0, device=local, lane_offset=rank * n, precision=a.precision, block_size=a.block,
+                         **phys)
+        hpool = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
+        step = lambda s: env.step(hpool[s % 16], pool[s % 16], autoreset=True)
+    else:
+        from ilrl_amd.clips import CLIP_NAMES
+        clips = tuple(CLIP_NAMES) if a.clip == "all" else (a.clip,)
+        env = HumanoidVecEnv(n, clips=clips, seed=0, device=local, lane_offset=rank * n, precision=a.precision,
+                             block_size=a.block, **phys)
+        step = lambda s: env.step(pool[s % 16], autoreset=True)
+    env.reset()
     for w in range(a.warmup):
-        env.step(pool[w % 16], autoreset=True)
+        step(w)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -105,7 +119,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record()
     for s in range(a.steps):
-        env.step(pool[s % 16], autoreset=True)
+        step(s)
     ev1.record()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -138,18 +152,23 @@ def main():
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": wall_max / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
-            "config": {"workload": "HumanoidBulletEnv-v0-Low step+reward, %s, %d envs/GPU, uniform random actions, "
-                                   "auto-reset" % (a.clip, n), "envs_per_gpu": n, "clip": a.clip,
+            "config": {"workload": ("HumanoidBulletEnv-v0-Hier two-level rollout (high heading every 5 low steps), "
+                                    if a.hier else "HumanoidBulletEnv-v0-Low step+reward, ") +
+                                   "%s, %d envs/GPU, uniform random actions, auto-reset" % (a.clip, n),
+                       "envs_per_gpu": n, "clip": a.clip,
                        "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_env_step": bpl, "kernel_ms": kern_ms},
             "error_flags": flags,
         }
+        if a.hier:
+            out["metric"] = "agent transitions/sec at N parallel hierarchical humanoids (5 of 6 are physics env steps)"
+            out["unit"] = "agent-steps/s"
         pp = os.path.join(REPO, "profiles", "parity_fp32_kernel1.json")   # written by tests/test_gpu_parity.py
-        if a.precision == "fp32" and os.path.exists(pp):
+        if a.precision == "fp32" and os.path.exists(pp) and not a.hier:
             out["parity"] = dict(json.load(open(pp)), source="profiles/parity_fp32_kernel1.json")
-        if world == 1 and a.cpu_seconds > 0:
+        if world == 1 and a.cpu_seconds > 0 and not a.hier:
             workers = a.cpu_workers or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, workers)
         print(json.dumps(out), flush=True)

@@ -44,6 +44,9 @@ struct Book {   // per-lane bookkeeping (mirrors HUM_BK_* in include/humanoid_en
     double target[3], srp[3], robot_pos[3], sep[3];
     double hldt, wt[2], lts;
     double dj, dvj, bps, es, jls, alive, dlts;
+    // hierarchical env (hier_env.py): level counter, agent expected next, high-level scores, body_xyz[0:2]
+    int level_rem, n_high, expect_high;
+    double hts, cum_drift, drift, dhts, cum_alive, bxy[2];
 };
 
 // --------------------------------------------------------------------------------------- helpers
@@ -178,6 +181,10 @@ __device__ inline void inc_frame(Book& b, const ClipDev& c, int inc) {   // :218
     if (b.frame == 0) {
         b.sep[0] = b.robot_pos[0]; b.sep[1] = b.robot_pos[1]; b.sep[2] = b.robot_pos[2];
     }
+}
+
+__device__ inline double dot3_blas(double x0, double x1, double x2, double y0, double y1, double y2) {   // np.dot
+    return fma(x2, y2, fma(x1, y1, x0 * y0));
 }
 
 __device__ inline void set_walk_target_hl(Book& b) {   // tail of checkTarget (:431-434)

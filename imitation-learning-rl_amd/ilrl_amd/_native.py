@@ -8,8 +8,10 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
-HUM_ABI_VERSION = 2   # include/humanoid_env.h
-HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 32, 12
+HUM_ABI_VERSION = 3   # include/humanoid_env.h
+HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 12
+HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
+HUM_AGENT_HIGH, HUM_AGENT_LOW = 1, 2
 HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS = 1, 2
 HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
 HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW = 1, 2, 4
@@ -18,7 +20,10 @@ HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW = 1, 2
 BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, target=4, starting_robot_pos=7,
           robot_pos=10, starting_ep_pos=13, highLevelDegTarget=16, walk_target=17, lowTargetScore=19,
           deltaJoints=20, deltaVelJoints=21, bodyPostureScore=22, electricityScore=23, jointLimitScore=24,
-          aliveReward=25, delta_lowTargetScore=26, clip=27, mode=28, rng_key_lo=29, rng_key_hi=30)
+          aliveReward=25, delta_lowTargetScore=26, clip=27, mode=28, rng_key_lo=29, rng_key_hi=30,
+          # hierarchical env (hier_env.py)
+          steps_remaining_at_level=31, num_high_level_steps=32, expect_high=33, highTargetScore=34,
+          cumulative_driftScore=35, driftScore=36, delta_highTargetScore=37, cumulative_aliveReward=38, body_xy=39)
 AUX = ["deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bodyPostureScore", "highTargetScore",
        "driftScore", "baseReward", "aliveReward", "electricityScore", "jointLimitScore", "dist_from_origin"]
 
@@ -26,7 +31,7 @@ AUX = ["deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bod
 EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_create", "hum_destroy", "hum_set_clip",
            "hum_set_lane_clips", "hum_set_lane_modes", "hum_set_predefined_targets", "hum_reset", "hum_step",
            "hum_step_graph", "hum_get_aux", "hum_get_state", "hum_set_state", "hum_get_parts",
-           "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream"]
+           "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step"]
 
 
 class HumConfig(ctypes.Structure):
@@ -39,7 +44,7 @@ class HumConfig(ctypes.Structure):
                 ("limit_max_impulse", ctypes.c_double), ("max_coord_vel", ctypes.c_double),
                 ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
                 ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32),
-                ("envs_per_block", ctypes.c_int32)]
+                ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32)]
 
 
 class NativeError(RuntimeError):
@@ -72,6 +77,8 @@ def lib():
     L.hum_set_predefined_targets.argtypes = [vp, dp, i32]
     L.hum_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hum_step.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, vp]
+    L.hum_hier_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.hum_hier_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp]
     L.hum_step_graph.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, i32]
     L.hum_get_aux.argtypes = [vp, vp, vp]
     L.hum_get_state.argtypes = [vp, dp, dp]

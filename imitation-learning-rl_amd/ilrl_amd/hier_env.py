@@ -1,0 +1,290 @@
+"""Drop-in Python surface for the reference's two-level env, backed by the same HIP kernel (no CPU fallback).
+
+* `HierVecEnv` - N device-resident lanes of `HierarchicalHumanoidEnv` (hier_env.py:38-641) on one GPU; one
+  `hum_hier_step` launch advances every lane by one agent transition: lanes whose acting agent is the high level
+  run high_level_step (heading -> walk target, no physics), the others low_level_step (4 physics substeps +
+  imitation reward + level hand-back every 5 steps).
+* `HierarchicalHumanoidEnv` - the reference's single-env MultiAgentEnv view (reset() / resetFromFrame() /
+  step(action_dict, debug)) returning the same {"high_level_agent": ..., "low_level_agent": ...} dicts, with
+  the reference's attribute names (target, robot_pos, highTargetScore, driftScore, steps_remaining_at_level, ...).
+* `HierarchicalVectorEnv` - RLlib 1.2 has no vectorised MultiAgentEnv, so the drop-in for N lanes is a
+  `BaseEnv` (poll / send_actions / try_reset / get_unwrapped) over one HierVecEnv.
+* `make_env_hier`, `register_envs` - train_config.py:18-20,320.
+
+ray is optional (absent in this image): BaseEnv is subclassed only when importable.
+"""
+import numpy as np
+
+from . import _native as N
+from .low_level_env import _box, _BookView
+from .vec_env import HumanoidVecEnv, _ptr
+
+ENV_HIER = "HumanoidBulletEnv-v0-Hier"
+HIGH, LOW = "high_level_agent", "low_level_agent"
+HIER_CLIP = "motion09_03"   # motion_list[selected_motion] (hier_env.py:50,170)
+
+HIGH_OBS_SPACE = lambda: _box(-np.inf, np.inf, (8 + 17 * 2 + 2,))      # hier_env.py:52
+HIGH_ACT_SPACE = lambda: _box(-1.0, 1.0, (2,))                          # :53-55
+LOW_OBS_SPACE = lambda: _box(-np.inf, np.inf, (8 + 17 * 2 + 14 * 2,))   # :57
+LOW_ACT_SPACE = lambda: _box(-1.0, 1.0, (17,))                          # :58
+
+
+class HierVecEnv(HumanoidVecEnv):
+    """N lanes of HierarchicalHumanoidEnv behind hum_hier_reset / hum_hier_step (include/humanoid_env.h)."""
+
+    def __init__(self, n, clip=HIER_CLIP, seed=0, device=0, lane_offset=0, precision="fp32", **physics):
+        super().__init__(n, clips=(clip,), seed=seed, device=device, lane_offset=lane_offset, precision=precision,
+                         hier=1, **physics)
+        t, f32 = self.torch, self.torch.float32
+        self.obs_high = t.zeros(self.n, N.HUM_NOBS_HIGH, dtype=f32, device=self.device)
+        self.obs_high_reset = t.zeros(self.n, N.HUM_NOBS_HIGH, dtype=f32, device=self.device)
+        self.reward_high = t.zeros(self.n, dtype=f32, device=self.device)
+        self.agents = t.zeros(self.n, dtype=t.uint8, device=self.device)
+        self._zero_high = t.zeros(self.n, N.HUM_NACT_HIGH, dtype=f32, device=self.device)
+        self._zero_low = t.zeros(self.n, N.HUM_NACT, dtype=f32, device=self.device)
+
+    def reset(self, mask=None, start_frame=None, reset_yaw=None):
+        """reset() (start_frame None: startFrame and resetYaw drawn per lane) or resetFromFrame(); -> [n,44]."""
+        t = self.torch
+        m = None if mask is None else t.as_tensor(mask, dtype=t.uint8, device=self.device).contiguous()
+        sf = None if start_frame is None else t.as_tensor(start_frame, dtype=t.int32, device=self.device).expand(self.n).contiguous()
+        ry = None if reset_yaw is None else t.as_tensor(reset_yaw, dtype=t.float64, device=self.device).expand(self.n).contiguous()
+        N.check(N.lib().hum_hier_reset(self.h, _ptr(m), _ptr(sf), _ptr(ry), _ptr(self.obs_high), self._stream()),
+                "hum_hier_reset")
+        return self.obs_high
+
+    def _act(self, a, width, zero):
+        if a is None:
+            return zero
+        t = self.torch
+        a = t.as_tensor(a, dtype=t.float32, device=self.device).contiguous()
+        if a.shape != (self.n, width):
+            raise ValueError("actions must be [%d, %d], got %s" % (self.n, width, tuple(a.shape)))
+        return a
+
+    def step(self, high_actions=None, low_actions=None, agent=None, autoreset=False, skip_physics=False):
+        """One agent transition per lane.  Returns (agents, obs_high, obs_low, rew_high, rew_low, done, frame)."""
+        t = self.torch
+        ah = self._act(high_actions, N.HUM_NACT_HIGH, self._zero_high)
+        al = self._act(low_actions, N.HUM_NACT, self._zero_low)
+        ag = None if agent is None else t.as_tensor(agent, dtype=t.uint8, device=self.device).expand(self.n).contiguous()
+        flags = (N.HUM_STEP_AUTORESET if autoreset else 0) | (N.HUM_STEP_SKIP_PHYSICS if skip_physics else 0)
+        N.check(N.lib().hum_hier_step(self.h, _ptr(ah), _ptr(al), _ptr(ag), _ptr(self.agents), _ptr(self.obs_high),
+                                      _ptr(self.obs), _ptr(self.reward_high), _ptr(self.reward), _ptr(self.done),
+                                      _ptr(self.frame), flags, _ptr(self.obs_high_reset), self._stream()),
+                "hum_hier_step")
+        return self.agents, self.obs_high, self.obs, self.reward_high, self.reward, self.done, self.frame
+
+
+class _HierBookView(_BookView):
+    _HIER_SCALARS = {"selected_motion_frame": ("frame", int), "steps_remaining_at_level": (None, int),
+                     "num_high_level_steps": (None, int), "highTargetScore": (None, float),
+                     "driftScore": (None, float), "cumulative_driftScore": (None, float),
+                     "delta_highTargetScore": (None, float), "cumulative_aliveReward": (None, float)}
+
+    def __getattr__(self, name):
+        if name in _HierBookView._HIER_SCALARS:
+            key, typ = _HierBookView._HIER_SCALARS[name]
+            return typ(self._book()[N.BK[key or name]])
+        return _BookView.__getattr__(self, name)
+
+
+class HierarchicalHumanoidEnv(_HierBookView):
+    """Single-env MultiAgentEnv view (1 lane) with the reference signature (hier_env.py:43)."""
+
+    metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 60}
+
+    def __init__(self, customRobot=None, seed=0, device=0, precision="fp32", **physics):
+        self.__dict__["_v"] = HierVecEnv(1, seed=seed, device=device, precision=precision, **physics)
+        self.__dict__["_cache"] = None
+        self.__dict__["_debug"] = False
+        self.__dict__["_pred_on"] = False
+        self.__dict__["_pred"] = np.array([[]])
+        self.high_level_obs_space = HIGH_OBS_SPACE()
+        self.high_level_act_space = HIGH_ACT_SPACE()
+        self.low_level_obs_space = LOW_OBS_SPACE()
+        self.low_level_act_space = LOW_ACT_SPACE()
+        self.motion_list = ["motion08_03", "motion09_03"]
+        self.selected_motion = 1
+        self.step_per_level = 5
+        self.max_timestep = 3000
+        self.skipFrame = 2
+        self.targetLen = 5
+        self.low_level_agent_id = LOW
+
+    def __setattr__(self, name, value):
+        if name == "usePredefinedTarget":
+            self.__dict__["_pred_on"] = bool(value)
+            self._v.set_modes(debug=self._debug, predefined=self._pred_on)
+        elif name == "predefinedTarget":
+            arr = np.asarray(value, dtype=np.float64)
+            self.__dict__["_pred"] = arr
+            if arr.size:
+                self._v.set_predefined_targets(arr.reshape(-1, 3))
+        else:
+            self.__dict__[name] = value
+
+    @property
+    def usePredefinedTarget(self):
+        return self._pred_on
+
+    @property
+    def predefinedTarget(self):
+        return self._pred
+
+    def _book(self):
+        if self._cache is None:
+            self.__dict__["_cache"] = self._v.get_state()[1][0]
+        return self._cache
+
+    def reset(self):                                                    # hier_env.py:235-243
+        self.__dict__["_cache"] = None
+        return {HIGH: self._v.reset()[0].double().cpu().numpy()}
+
+    def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :259-319
+        if not (startFromRef and initVel):
+            raise NotImplementedError("resetFromFrame supports startFromRef=True, initVel=True (all reference callers)")
+        self.__dict__["_cache"] = None
+        return {HIGH: self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw))[0].double().cpu().numpy()}
+
+    def step(self, action_dict, debug=False):                           # :355-366
+        assert len(action_dict) == 1, action_dict
+        if bool(debug) != self._debug:
+            self.__dict__["_debug"] = bool(debug)
+            self._v.set_modes(debug=self._debug, predefined=self._pred_on)
+        if HIGH in action_dict:
+            ah = np.asarray(action_dict[HIGH], dtype=np.float32).reshape(1, 2)
+            out = self._v.step(high_actions=ah, agent=1)
+        else:
+            al = np.asarray(list(action_dict.values())[0], dtype=np.float32).reshape(1, 17)
+            assert np.isfinite(al).all()                                # humanoid.py:55
+            out = self._v.step(low_actions=al, agent=0)
+        agents, oh, ol, rh, rl, done, _ = [x.cpu().numpy() for x in out]
+        self.__dict__["_cache"] = None
+        obs, rew = {}, {}
+        if agents[0] & N.HUM_AGENT_HIGH:
+            obs[HIGH] = oh[0].astype(np.float64)
+            rew[HIGH] = float(rh[0])
+        if agents[0] & N.HUM_AGENT_LOW:
+            obs[LOW] = ol[0].astype(np.float64)
+            rew[LOW] = float(rl[0])
+        return obs, rew, {"__all__": bool(done[0])}, {}
+
+    def close(self):
+        self._v.close()
+
+    def render(self, mode="human"):
+        raise NotImplementedError("rendering is out of scope (env_vis_hier.py)")
+
+
+class HierLaneView(_HierBookView):
+    def __init__(self, venv, i):
+        self.__dict__["_venv"] = venv
+        self.__dict__["_i"] = i
+
+    def _book(self):
+        return self._venv._books()[self._i]
+
+
+def _base_env_cls():
+    try:
+        from ray.rllib.env.base_env import BaseEnv
+        return BaseEnv
+    except Exception:
+        return object
+
+
+class HierarchicalVectorEnv(_base_env_cls()):
+    """RLlib 1.2 BaseEnv over N hierarchical lanes (one hum_hier_step launch per send_actions/poll round).
+
+    poll() -> (obs, rewards, dones, infos, off_policy_actions) as {env_id: {agent_id: ...}} with
+    dones[env_id]["__all__"]; send_actions({env_id: {agent_id: action}}); done lanes are reset inside the step
+    launch and try_reset(env_id) serves the reset observation {"high_level_agent": obs}.
+    """
+
+    def __init__(self, num_envs, seed=0, device=0, precision="fp32", **physics):
+        self.venv = HierVecEnv(num_envs, seed=seed, device=device, precision=precision, **physics)
+        self.num_envs = num_envs
+        self._views = [HierLaneView(self, i) for i in range(num_envs)]
+        self._book_cache = None
+        self._pending = None
+        self._reset_obs = None
+        self._reset_pending = np.zeros(num_envs, dtype=bool)
+
+    def _books(self):
+        if self._book_cache is None:
+            self._book_cache = self.venv.get_state()[1]
+        return self._book_cache
+
+    def _first_poll(self):
+        oh = self.venv.reset().cpu().numpy().astype(np.float64)
+        self._book_cache = None
+        obs = {i: {HIGH: oh[i]} for i in range(self.num_envs)}
+        return obs, {i: {HIGH: 0.0} for i in range(self.num_envs)}, \
+            {i: {"__all__": False} for i in range(self.num_envs)}, {i: {HIGH: {}} for i in range(self.num_envs)}
+
+    def poll(self):
+        if self._pending is None:
+            obs, rew, dones, infos = self._first_poll()
+        else:
+            obs, rew, dones, infos = self._pending
+        self._pending = ({}, {}, {}, {})
+        return obs, rew, dones, infos, {}
+
+    def send_actions(self, action_dict):
+        n = self.num_envs
+        ah = np.zeros((n, 2), np.float32)
+        al = np.zeros((n, 17), np.float32)
+        agent = np.zeros(n, np.uint8)
+        for i, ad in action_dict.items():
+            assert len(ad) == 1, ad
+            if HIGH in ad:
+                ah[i] = ad[HIGH]
+                agent[i] = 1
+            else:
+                al[i] = list(ad.values())[0]
+        if not np.isfinite(al).all():
+            raise AssertionError("non-finite action (humanoid.py:55)")
+        agents, oh, ol, rh, rl, done, _ = [x.cpu().numpy() for x in
+                                           self.venv.step(ah, al, agent=agent, autoreset=True)]
+        self._reset_obs = self.venv.obs_high_reset.cpu().numpy().astype(np.float64)
+        self._reset_pending = done.astype(bool).copy()
+        self._book_cache = None
+        obs, rew, dones, infos = {}, {}, {}, {}
+        for i in action_dict:
+            o, r = {}, {}
+            if agents[i] & N.HUM_AGENT_HIGH:
+                o[HIGH] = oh[i].astype(np.float64)
+                r[HIGH] = float(rh[i])
+            if agents[i] & N.HUM_AGENT_LOW:
+                o[LOW] = ol[i].astype(np.float64)
+                r[LOW] = float(rl[i])
+            obs[i], rew[i], dones[i], infos[i] = o, r, {"__all__": bool(done[i])}, {k: {} for k in o}
+        self._pending = (obs, rew, dones, infos)
+
+    def try_reset(self, env_id):
+        if self._reset_pending[env_id]:
+            self._reset_pending[env_id] = False
+            return {HIGH: self._reset_obs[env_id]}
+        mask = np.zeros(self.num_envs, dtype=np.uint8)
+        mask[env_id] = 1
+        self._book_cache = None
+        return {HIGH: self.venv.reset(mask=mask)[env_id].cpu().numpy().astype(np.float64)}
+
+    def get_unwrapped(self):
+        return self._views
+
+    def stop(self):
+        self.venv.close()
+
+
+def make_env_hier(env_config=None):
+    """train_config.py:18-20 (env_config ignored like the reference)."""
+    return HierarchicalHumanoidEnv()
+
+
+def register_envs():
+    """register_env(ENV_HIER, make_env_hier) (train_config.py:320) when Ray is importable."""
+    from ray.tune.registry import register_env
+    register_env(ENV_HIER, make_env_hier)
+    return ENV_HIER

@@ -2,7 +2,9 @@
  *
  * Drop-in boundary for the reference hot path `LowLevelHumanoidEnv.reset()/step()`
  * (/root/reference/low_level_env.py:36-526, registered as "HumanoidBulletEnv-v0-Low" by
- * train_config.py:29,321).  One handle = N independent env lanes resident on ONE GPU, advanced by one
+ * train_config.py:29,321) and its two-level counterpart `HierarchicalHumanoidEnv.reset()/step()`
+ * (/root/reference/hier_env.py:38-641, "HumanoidBulletEnv-v0-Hier", train_config.py:18-20,320), selected
+ * per handle by hum_config.hier.  One handle = N independent env lanes resident on ONE GPU, advanced by one
  * HIP kernel launch per env step.  The Python mirror (`ilrl_amd.low_level_env`) binds this header with
  * ctypes; INTEGRATION.md shows the binding a maintainer adds on the reference side.
  *
@@ -32,11 +34,13 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 2
+#define HUM_ABI_VERSION 3
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
-#define HUM_NBOOK 32    /* bookkeeping doubles per lane, layout HUM_BK_* below */
+#define HUM_NBOOK 48    /* bookkeeping doubles per lane, layout HUM_BK_* below */
+#define HUM_NOBS_HIGH 44   /* high_level_obs_space shape, hier_env.py:52 */
+#define HUM_NACT_HIGH 2    /* high_level_act_space shape (cos, sin of the heading), hier_env.py:53-55 */
 #define HUM_NAUX 12     /* RewardLogCallback terms per lane, layout HUM_AUX_* below */
 #define HUM_MAX_CLIPS 8
 
@@ -69,8 +73,18 @@ enum {
     HUM_BK_JOINT_LIMIT = 24, HUM_BK_ALIVE = 25, HUM_BK_DELTA_LOW_TARGET = 26, HUM_BK_CLIP = 27,
     HUM_BK_MODE = 28,
     /* 64-bit RNG stream key as two u32 halves; initialised to splitmix64(seed + lane_offset + lane) */
-    HUM_BK_RNG_KEY_LO = 29, HUM_BK_RNG_KEY_HI = 30
+    HUM_BK_RNG_KEY_LO = 29, HUM_BK_RNG_KEY_HI = 30,
+    /* hierarchical env only (hier_env.py): steps_remaining_at_level, num_high_level_steps, the agent expected
+       to act next (1 = high), highTargetScore, cumulative_driftScore, driftScore, delta_highTargetScore,
+       cumulative_aliveReward, flat_env.robot.body_xyz[0:2] of the last calc_state */
+    HUM_BK_LEVEL_REMAINING = 31, HUM_BK_NUM_HIGH_STEPS = 32, HUM_BK_EXPECT_HIGH = 33, HUM_BK_HIGH_TARGET_SCORE = 34,
+    HUM_BK_CUM_DRIFT = 35, HUM_BK_DRIFT = 36, HUM_BK_DELTA_HIGH_TARGET = 37, HUM_BK_CUM_ALIVE = 38,
+    HUM_BK_BODY_XY /* 2 */ = 39
 };
+
+/* hum_hier_step per-lane agent mask (which entries of the reference's obs/rew dicts are present) */
+#define HUM_AGENT_HIGH 1u   /* "high_level_agent" obs + reward */
+#define HUM_AGENT_LOW 2u    /* "low_level_agent" obs + reward */
 
 /* aux (RewardLogCallback, custom_callback.py:43-80) layout, float32 */
 enum {
@@ -100,6 +114,8 @@ typedef struct hum_config {
     int32_t self_collision;   /* 1 */
     int32_t joint_damping;    /* 1 = implicit MJCF joint damping */
     int32_t kernel;           /* 1 = cooperative (16 lanes/env, LDS-resident; default), 0 = one env per lane */
+    int32_t hier;             /* 0 = LowLevelHumanoidEnv semantics (hum_reset/hum_step), 1 = HierarchicalHumanoidEnv
+                                 (hum_hier_reset/hum_hier_step; clip = the selected motion, motion09_03) */
     int32_t envs_per_block;   /* cooperative kernel: envs per wavefront-block (4 = 64 threads (default), 2 = 32,
                                  1 = 16).  Fewer envs per wave buys SIMD co-residency but multiplies the wave
                                  instruction stream per env: measured 0.39 / 0.64 / 0.98 ms at 4096 envs */
@@ -147,6 +163,40 @@ int hum_step(hum_env* env, const float* actions, float* obs, float* reward, uint
  * own stream (hum_stream()); inputs must be ready (synchronise the producing stream first). */
 int hum_step_graph(hum_env* env, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
                    uint32_t flags, float* obs_reset, int32_t k);
+
+/* HierarchicalHumanoidEnv.reset()/resetFromFrame() (hier_env.py:235-319) for masked lanes (hier handles only):
+ * start_frame NULL = reset(): draw startFrame then resetYaw from the lane RNG (:239-240); given = resetFromFrame
+ * with reset_yaw_deg (NULL = 0).  high_obs_out: device float32 [n,44] = {"high_level_agent": obs}. */
+int hum_hier_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+                   float* high_obs_out, void* stream);
+
+/* HierarchicalHumanoidEnv.step(action_dict) (hier_env.py:355-366, 538-641) for all lanes: each lane applies the
+ * action of the agent it expects (the one that received an observation; `agent` (device u8 [n], 1 = high, 0 = low)
+ * overrides it, NULL = expected): high_act [n,2] f32 -> high_level_step (no physics), low_act [n,17] f32 ->
+ * low_level_step.  Outputs: agents [n] u8 (HUM_AGENT_* bits present in the reference's returned dicts),
+ * high_obs [n,44] / low_obs [n,70] (rows written only where present), high_rew / low_rew [n] (0 where absent),
+ * done [n] u8 (done["__all__"]), frame [n] i32 (may be NULL).  HUM_STEP_AUTORESET resets done lanes in the
+ * same launch and writes their new high-level obs to high_obs_reset ([n,44], may be NULL). */
+int hum_hier_step(hum_env* env, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
+                  float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
+                  uint32_t flags, float* high_obs_reset, void* stream);
+
+/* HierarchicalHumanoidEnv.reset()/resetFromFrame() (hier_env.py:235-319) for masked lanes (hier handles only):
+ * start_frame NULL = reset(): draw startFrame then resetYaw from the lane RNG (:239-240); given = resetFromFrame
+ * with reset_yaw_deg (NULL = 0).  high_obs_out: device float32 [n,44] = {"high_level_agent": obs}. */
+int hum_hier_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+                   float* high_obs_out, void* stream);
+
+/* HierarchicalHumanoidEnv.step(action_dict) (hier_env.py:355-366, 538-641) for all lanes: each lane applies the
+ * action of the agent it expects (the one that received an observation; `agent` (device u8 [n], 1 = high, 0 = low)
+ * overrides it, NULL = expected): high_act [n,2] f32 -> high_level_step (no physics), low_act [n,17] f32 ->
+ * low_level_step.  Outputs: agents [n] u8 (HUM_AGENT_* bits present in the reference's returned dicts),
+ * high_obs [n,44] / low_obs [n,70] (rows written only where present), high_rew / low_rew [n] (0 where absent),
+ * done [n] u8 (done["__all__"]), frame [n] i32 (may be NULL).  HUM_STEP_AUTORESET resets done lanes in the
+ * same launch and writes their new high-level obs to high_obs_reset ([n,44], may be NULL). */
+int hum_hier_step(hum_env* env, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
+                  float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
+                  uint32_t flags, float* high_obs_reset, void* stream);
 
 /* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
 int hum_get_aux(hum_env* env, float* aux_out, void* stream);

@@ -1,0 +1,217 @@
+"""GPU parity for the hierarchical env (hum_hier_reset / hum_hier_step) against the reference's golden vectors
+(tests/golden/make_golden_hier.py imports the real hier_env.py) and the CPU oracle (oracle/oracle_hier.py).
+
+Each golden scenario is replayed as ONE launch with one lane per recorded call: lane t gets the physics state
+and bookkeeping the reference held before call t and the agent/action it received.
+* injected physics (HUM_STEP_SKIP_PHYSICS, lane physics = the reference's post-call state): env logic must equal
+  the reference's - agents present in the returned dicts, done, frame, level counter and RNG use bit-exact;
+  fp64 kernel: obs within 1 float32 ulp, rewards 1e-6; fp32 kernel: obs 2e-5, rewards 1e-4;
+* full physics (fp64): kernel physics vs the fp64 oracle physics, state within 1e-6.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import oracle_hier as OH
+from golden_replay import rec
+from test_oracle_golden_hier import HIER_SCEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from ilrl_amd import _native as N  # noqa: E402
+from ilrl_amd.clips import load_clip  # noqa: E402
+from ilrl_amd.hier_env import HIGH, LOW, HierarchicalHumanoidEnv, HierarchicalVectorEnv, HierVecEnv  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def golden_hier():
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_hier.npz"),
+                   allow_pickle=False)
+
+
+def book_rows(r):
+    """HUM_NBOOK rows with the reference bookkeeping BEFORE each recorded call."""
+    seed, lane, _, debug, _, _, _ = [int(x) for x in r["meta"]]
+    key = O.splitmix64((seed + lane) & O.M64)
+    T = len(r["done"])
+    out = np.zeros((T, N.HUM_NBOOK))
+    for t in range(T):
+        src = (lambda k: r["book0_" + k]) if t == 0 else (lambda k: r["book_" + k][t - 1])
+        b = out[t]
+        b[N.BK["frame"]] = src("selected_motion_frame")
+        b[N.BK["cur_timestep"]] = r["cur_timestep_pre"][t]
+        b[N.BK["rng_counter"]] = src("rng_counter")
+        b[N.BK["predefinedTargetIndex"]] = src("predefinedTargetIndex")
+        for k in ("target", "starting_robot_pos", "robot_pos", "starting_ep_pos"):
+            b[N.BK[k]:N.BK[k] + 3] = src(k)
+        b[N.BK["walk_target"]:N.BK["walk_target"] + 2] = src("walk_target")
+        b[N.BK["body_xy"]:N.BK["body_xy"] + 2] = src("body_xyz")
+        for k in ("highLevelDegTarget", "lowTargetScore", "deltaJoints", "deltaVelJoints", "bodyPostureScore",
+                  "electricityScore", "jointLimitScore", "aliveReward", "delta_lowTargetScore", "highTargetScore",
+                  "driftScore", "cumulative_driftScore", "delta_highTargetScore", "cumulative_aliveReward",
+                  "steps_remaining_at_level", "num_high_level_steps"):
+            b[N.BK[k]] = src(k)
+        b[N.BK["expect_high"]] = r["agent"][t]
+        b[N.BK["clip"]] = 0
+        b[N.BK["mode"]] = (N.HUM_MODE_DEBUG if debug else 0) | (N.HUM_MODE_PREDEFINED if len(r["predefined"]) else 0)
+        b[N.BK["rng_key_lo"]] = key & 0xFFFFFFFF
+        b[N.BK["rng_key_hi"]] = key >> 32
+    return out
+
+
+def run_scenario(r, precision, skip_physics, kernel=1):
+    T = len(r["done"])
+    env = HierVecEnv(T, precision=precision, kernel=kernel)
+    if len(r["predefined"]):
+        env.set_predefined_targets(r["predefined"])
+    phys = r["state_post"] if skip_physics else r["state_pre"]
+    env.set_state(phys, book_rows(r))
+    agents, oh, ol, rh, rl, done, frame = env.step(r["action_high"], r["action_low"], skip_physics=skip_physics)
+    out = dict(agents=agents.cpu().numpy(), oh=oh.cpu().numpy(), ol=ol.cpu().numpy(), rh=rh.cpu().numpy(),
+               rl=rl.cpu().numpy(), done=done.cpu().numpy().astype(bool), frame=frame.cpu().numpy())
+    out["phys"], out["book"] = env.get_state()
+    env.close()
+    return out
+
+
+def f32_ulp_diff(a, b):
+    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b)
+
+
+def check_env_logic(o, r, precision):
+    hh, hl = r["has_high"].astype(bool), r["has_low"].astype(bool)
+    np.testing.assert_array_equal(o["agents"], hh * N.HUM_AGENT_HIGH + hl * N.HUM_AGENT_LOW)
+    np.testing.assert_array_equal(o["done"], r["done"])
+    np.testing.assert_array_equal(o["frame"], r["book_selected_motion_frame"].astype(np.int32))
+    for k in ("cur_timestep", "rng_counter", "steps_remaining_at_level", "num_high_level_steps",
+              "predefinedTargetIndex"):
+        np.testing.assert_array_equal(o["book"][:, N.BK[k]], r["book_" + k], err_msg=k)
+    if precision == "fp64":
+        assert f32_ulp_diff(o["oh"][hh], r["obs_high"][hh]).max(initial=0) <= 1, "high obs beyond 1 f32 ulp"
+        assert f32_ulp_diff(o["ol"][hl], r["obs_low"][hl]).max(initial=0) <= 1, "low obs beyond 1 f32 ulp"
+        rtol = 1e-6
+    else:
+        np.testing.assert_allclose(o["oh"][hh], r["obs_high"][hh], rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose(o["ol"][hl], r["obs_low"][hl], rtol=2e-5, atol=2e-5)
+        rtol = 1e-4
+    np.testing.assert_allclose(o["rh"], r["rew_high"], rtol=rtol, atol=rtol)
+    np.testing.assert_allclose(o["rl"], r["rew_low"], rtol=rtol, atol=rtol)
+    btol = 1e-12 if precision == "fp64" else 1e-5
+    for k in ("target", "starting_robot_pos", "robot_pos"):
+        np.testing.assert_allclose(o["book"][:, N.BK[k]:N.BK[k] + 3], r["book_" + k], rtol=0, atol=btol, err_msg=k)
+    # highLevelDegTarget goes through the float32 arctan2 of the high action (hier_env.py:540)
+    np.testing.assert_allclose(o["book"][:, N.BK["highLevelDegTarget"]], r["book_highLevelDegTarget"], rtol=0,
+                               atol=1e-6)
+    for k in ("highTargetScore", "driftScore", "cumulative_driftScore", "delta_highTargetScore",
+              "cumulative_aliveReward", "deltaJoints", "deltaVelJoints", "bodyPostureScore", "electricityScore",
+              "jointLimitScore", "aliveReward"):
+        np.testing.assert_allclose(o["book"][:, N.BK[k]], r["book_" + k], rtol=1e-6, atol=max(btol, 1e-9), err_msg=k)
+
+
+@pytest.mark.parametrize("kernel", [1, 0])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+@pytest.mark.parametrize("name", HIER_SCEN)
+def test_hier_env_logic_matches_reference(golden_hier, name, precision, kernel):
+    r = rec(golden_hier, name)
+    o = run_scenario(r, precision, skip_physics=True, kernel=kernel)
+    check_env_logic(o, r, precision)
+
+
+@pytest.mark.parametrize("kernel", [1, 0])
+@pytest.mark.parametrize("name", HIER_SCEN)
+def test_hier_physics_fp64_matches_oracle(golden_hier, name, kernel):
+    r = rec(golden_hier, name)
+    o = run_scenario(r, "fp64", skip_physics=False, kernel=kernel)
+    err = np.abs(o["phys"] - r["state_post"])
+    assert err.max() < 1e-6, "max state err %.3g" % err.max()
+    np.testing.assert_array_equal(o["done"], r["done"])
+    hl = r["has_low"].astype(bool)
+    np.testing.assert_allclose(o["ol"][hl], r["obs_low"][hl], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(o["rl"], r["rew_low"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_hier_reset_matches_oracle(precision):
+    clip = load_clip("motion09_03")
+    n = 48
+    env = HierVecEnv(n, seed=77, precision=precision)
+    sf = np.where(np.arange(n) % 3 == 0, np.arange(n) % (clip.max_frame - 5), -1).astype(np.int32)
+    yaw = np.linspace(-60, 60, n)
+    oh = env.reset(start_frame=torch.as_tensor(sf, device="cuda"),
+                   reset_yaw=torch.as_tensor(yaw, device="cuda")).cpu().numpy()
+    phys, book = env.get_state()
+    for i in range(n):
+        o = OH.OracleHierEnv(clip, seed=77, lane=i)
+        ref = o.reset() if sf[i] < 0 else o.resetFromFrame(int(sf[i]), resetYaw=yaw[i])
+        assert book[i, N.BK["frame"]] == o.selected_motion_frame
+        assert book[i, N.BK["rng_counter"]] == o.rng.counter
+        np.testing.assert_allclose(book[i, N.BK["target"]:N.BK["target"] + 3], o.target, atol=1e-12)
+        np.testing.assert_allclose(phys[i], o.state, atol=1e-5 if precision == "fp32" else 1e-12, rtol=1e-6)
+        np.testing.assert_allclose(oh[i], ref[HIGH], atol=2e-5 if precision == "fp32" else 1e-6, rtol=1e-5)
+        assert book[i, N.BK["highTargetScore"]] == -5 and book[i, N.BK["expect_high"]] == 1
+    env.close()
+
+
+def test_hier_rollout_at_scale():
+    """4096 lanes x 120 auto-reset agent transitions with random high/low actions: protocol invariants."""
+    n = 4096
+    env = HierVecEnv(n, seed=3)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    n_high = 0
+    for t in range(120):
+        ah = torch.rand(n, 2, device="cuda", generator=g) * 2 - 1
+        al = (torch.rand(n, 17, device="cuda", generator=g) * 2 - 1) * 0.5
+        agents, oh, ol, rh, rl, done, frame = env.step(ah, al, autoreset=True)
+        a = agents.cpu().numpy()
+        assert (a != 0).all()
+        d = done.cpu().numpy().astype(bool)
+        assert ((a[d] & 3) == 3).all()          # episode end returns both agents' obs
+        n_high += int(((a & 1) != 0).sum())
+    torch.cuda.synchronize()
+    phys, book = env.get_state()
+    assert np.isfinite(phys).all() and torch.isfinite(rl).all() and torch.isfinite(rh).all()
+    rem = book[:, N.BK["steps_remaining_at_level"]]
+    assert ((rem >= 0) & (rem <= 5)).all()
+    assert n_high > 120 * n // 7
+    env.close()
+
+
+def test_hier_gym_view_and_base_env():
+    e = HierarchicalHumanoidEnv()
+    o = e.reset()
+    assert set(o) == {HIGH} and o[HIGH].shape == (44,)
+    obs, rew, done, info = e.step({HIGH: np.array([1.0, 0.0], np.float32)})
+    assert set(obs) == {LOW} and obs[LOW].shape == (70,) and rew == {LOW: 0.0} and done == {"__all__": False}
+    assert e.steps_remaining_at_level == 5 and e.num_high_level_steps == 1
+    seen_high = False
+    for _ in range(5):
+        obs, rew, done, info = e.step({LOW: np.zeros(17, np.float32)})
+        if done["__all__"]:
+            break
+        seen_high = seen_high or HIGH in obs
+    assert seen_high or done["__all__"]
+    for attr in ("highTargetScore", "driftScore", "robot_pos", "target", "selected_motion_frame", "cur_timestep"):
+        getattr(e, attr)
+    e.close()
+    v = HierarchicalVectorEnv(6)
+    obs, rew, dones, infos, _ = v.poll()
+    assert len(obs) == 6 and all(set(o) == {HIGH} for o in obs.values())
+    acts = {i: {HIGH: np.array([0.0, 1.0], np.float32)} for i in obs}
+    for _ in range(8):
+        v.send_actions(acts)
+        obs, rew, dones, infos, _ = v.poll()
+        acts = {}
+        for i, o in obs.items():
+            if dones[i]["__all__"]:
+                o = v.try_reset(i)
+            acts[i] = {HIGH: np.array([0.0, 1.0], np.float32)} if HIGH in o and LOW not in o or dones[i]["__all__"] \
+                else {LOW: np.zeros(17, np.float32)}
+    v.stop()
