@@ -1019,6 +1019,11 @@ int hum_hier_step(hum_env* e, const float* high_act, const float* low_act, const
 
 namespace {
 int launch_step(hum_env* e, const KArgs& a, hipStream_t s) {
+#ifdef HUM_DIAG_F32_ONLY   // diagnostic builds (phase timing): only the benchmarked kernel is instantiated
+    if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != 4)
+        return fail(HUM_ERR_ARG, "diagnostic build: only kernel 1, fp32, envs_per_block 4");
+    hipLaunchKernelGGL((step_group_kernel<float, 4>), dim3((e->n + 3) / 4), dim3(4 * GL), 0, s, a);
+#else
     if (e->cfg.kernel == 1) {
         const int epb = e->cfg.envs_per_block;
         const dim3 g((e->n + epb - 1) / epb), blk(epb * GL);
@@ -1035,6 +1040,7 @@ int launch_step(hum_env* e, const KArgs& a, hipStream_t s) {
         if (e->cfg.precision) hipLaunchKernelGGL(step_kernel<double>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
         else hipLaunchKernelGGL(step_kernel<float>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
     }
+#endif
     HIPCHK(hipGetLastError());
     return HUM_OK;
 }

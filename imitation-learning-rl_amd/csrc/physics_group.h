@@ -8,7 +8,7 @@
 //
 //   FK              every lane (registers), lane 0 publishes R/o/u to LDS
 //   ABA pass 1      lane b = body b: velocity, bias acceleration, spatial inertia, bias force
-//   ABA pass 2      body by body (leaves -> root), lanes split the 6k / k^2 / 21 matrix entries
+//   ABA pass 2      by tree level (4 steps, one body per 4-lane group), children summed by the parent
 //   ABA pass 3      every lane redundantly (tiny), lane 0 publishes accelerations
 //   limits/contacts lane-parallel candidate tests, ballot-compacted in the oracle's order
 //   rows            one constraint row per lane: Jacobian + test-impulse response M^-1 J^T
@@ -21,7 +21,8 @@ namespace hk {
 constexpr int GL = 16;                       // lanes per env
 constexpr int MAXC_G = 16;                   // contact cap of the cooperative kernel
 constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // 65 rows
-constexpr int RW = 2 * NV + 6;               // J[NV], M[NV], b, lo, hi, lam, meff, mu
+constexpr int RW = 2 * NV + 7;               // J[NV], M[NV], b, lo, hi, lam, meff, mu, 0 (pad read by lanes
+                                             // without a second nu component: branch-free PGS loads)
 constexpr int NCAND_GROUND = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 1 : 2; return n; }();
 constexpr int NCAND = NCAND_GROUND + NPAIR;
 
@@ -37,9 +38,17 @@ struct ModelTab {
     int gbody[NGEOM], gtype[NGEOM];
     T gr[NGEOM], gp1[NGEOM][3], gp2[NGEOM][3];
     int cand_a[NCAND], cand_b[NCAND];    // ground: (geom, endpoint) with cand_b = -1 - endpoint; pair: (ga, gb)
+    T gbr[NGEOM];                        // bounding-sphere radius about the segment midpoint: |p2-p1|/2 + r
     int act_dof[NACT];
     float act_gain[NACT];
 };
+
+constexpr double csqrt(double x) {   // constexpr Newton square root (model constants only)
+    if (x <= 0) return 0;
+    double r = x > 1 ? x : 1;
+    for (int i = 0; i < 100; i++) r = 0.5 * (r + x / r);
+    return r;
+}
 
 template <typename T>
 constexpr ModelTab<T> make_tab() {
@@ -69,6 +78,9 @@ constexpr ModelTab<T> make_tab() {
     for (int g = 0; g < NGEOM; g++) {
         m.gbody[g] = geom_body[g]; m.gtype[g] = geom_type[g]; m.gr[g] = (T)geom_r[g];
         for (int i = 0; i < 3; i++) { m.gp1[g][i] = (T)geom_p1[3 * g + i]; m.gp2[g][i] = (T)geom_p2[3 * g + i]; }
+        double h2 = 0;
+        for (int i = 0; i < 3; i++) h2 += (geom_p2[3 * g + i] - geom_p1[3 * g + i]) * (geom_p2[3 * g + i] - geom_p1[3 * g + i]);
+        m.gbr[g] = (T)(0.5 * csqrt(h2) + geom_r[g]);
         for (int e = 0; e < (geom_type[g] == 0 ? 1 : 2); e++) { m.cand_a[c] = g; m.cand_b[c] = -1 - e; c++; }
     }
     for (int k = 0; k < NPAIR; k++) { m.cand_a[c] = pair_a[k]; m.cand_b[c] = pair_b[k]; c++; }
@@ -274,6 +286,118 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
     }
 }
 
+// ------------------------------------------------------------------------- ABA pass 2, one tree level
+// Level tables (body per 4-lane group): children are always processed in an earlier level.
+constexpr int LVL_BODY[4][4] = {{4, 6, 8, 10}, {3, 5, 7, 9}, {2, 2, 2, 2}, {1, 1, 1, 1}};
+constexpr int LVL_KID[4][4][2] = {{{-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}},
+                                  {{4, -1}, {6, -1}, {8, -1}, {10, -1}},
+                                  {{3, 5}, {3, 5}, {3, 5}, {3, 5}},
+                                  {{2, -1}, {2, -1}, {2, -1}, {2, -1}}};
+template <int LV>
+__device__ inline int lvl_sel(int g, int (*f)(int)) {   // per-group compile-time value
+    const int v0 = f(LVL_BODY[LV][0]), v1 = f(LVL_BODY[LV][1]), v2 = f(LVL_BODY[LV][2]), v3 = f(LVL_BODY[LV][3]);
+    return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+}
+
+template <typename T, int LV>
+__device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt) {
+    const ModelTab<T>& M = tab<T>();
+    auto& A = S.x.aba;
+    const int b = lvl_sel<LV>(g, [](int x) { return x; });
+    const int k = lvl_sel<LV>(g, [](int x) { return body_ndof[x]; });
+    const int d0 = lvl_sel<LV>(g, [](int x) { return body_dof0[x]; });
+    T IA[21], pAb[6], cb[6], Sc[3][6], U[3][6], D[9], Di[9], uj[3], W[3][6];
+#pragma unroll
+    for (int q = 0; q < 21; q++) IA[q] = A.IA[b][q];
+#pragma unroll
+    for (int e = 0; e < 6; e++) { pAb[e] = A.pA[b][e]; cb[e] = A.c[b][e]; }
+    auto add_kid = [&](int kid) {
+#pragma unroll
+        for (int q = 0; q < 21; q++) IA[q] += A.IA[kid][q];
+#pragma unroll
+        for (int e = 0; e < 6; e++) pAb[e] += A.pA[kid][e];
+    };
+    // every group of a level has the same number of kids (0, 1 or 2)
+    if constexpr (LVL_KID[LV][0][0] >= 0)
+        add_kid(g == 0 ? LVL_KID[LV][0][0] : (g == 1 ? LVL_KID[LV][1][0] : (g == 2 ? LVL_KID[LV][2][0] : LVL_KID[LV][3][0])));
+    if constexpr (LVL_KID[LV][0][1] >= 0)
+        add_kid(g == 0 ? LVL_KID[LV][0][1] : (g == 1 ? LVL_KID[LV][1][1] : (g == 2 ? LVL_KID[LV][2][1] : LVL_KID[LV][3][1])));
+    const T ob[3] = {S.o[b][0], S.o[b][1], S.o[b][2]};
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const bool on = j < k;
+        const int d = on ? d0 + j : d0;
+        const T u[3] = {S.u[d][0], S.u[d][1], S.u[d][2]};
+        Sc[j][0] = on ? u[0] : T(0); Sc[j][1] = on ? u[1] : T(0); Sc[j][2] = on ? u[2] : T(0);
+        cross3(ob, Sc[j], Sc[j] + 3);
+        symmv(IA, Sc[j], U[j]);
+        T sp = 0;
+#pragma unroll
+        for (int e = 0; e < 6; e++) sp += Sc[j][e] * pAb[e];
+        T t = S.tau[d] - sp;
+        if (P.joint_damping) t -= M.damp[d] * S.nu[6 + d];
+        uj[j] = on ? t : T(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            T t = 0;
+#pragma unroll
+            for (int e = 0; e < 6; e++) t += Sc[i][e] * U[j][e];
+            D[3 * i + j] = t;
+        }
+        const bool on = i < k;
+        if (P.joint_damping) D[4 * i] += on ? dt * M.damp[on ? d0 + i : d0] : T(0);
+        D[4 * i] = on ? D[4 * i] : T(1);   // identity pivot for padded dofs
+    }
+    small_inverse<T, 3>(D, Di);
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int e = 0; e < 6; e++) {
+            T t = 0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) t += U[i][e] * Di[3 * i + j];
+            W[j][e] = t;
+        }
+    // Ia = IA - W U^T (in place), pa = pA + Ia c + W u
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int cc = r; cc < 6; cc++) {
+            T t = IA[sidx(r, cc)];
+#pragma unroll
+            for (int j = 0; j < 3; j++) t -= W[j][r] * U[j][cc];
+            IA[sidx(r, cc)] = t;
+        }
+    T pa[6];
+    symmv(IA, cb, pa);
+#pragma unroll
+    for (int e = 0; e < 6; e++) {
+        T t = pAb[e] + pa[e];
+#pragma unroll
+        for (int j = 0; j < 3; j++) t += W[j][e] * uj[j];
+        pa[e] = t;
+    }
+    // contribution to the parent in the body's own (now dead) slots; factorisation for passes 3 / responses.
+    // The 4 lanes of a group (and groups sharing a body) write identical values.
+#pragma unroll
+    for (int q = 0; q < 21; q++) A.IA[b][q] = IA[q];
+#pragma unroll
+    for (int e = 0; e < 6; e++) A.pA[b][e] = pa[e];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        if (j < k) {
+#pragma unroll
+            for (int e = 0; e < 6; e++) S.U[d0 + j][e] = U[j][e];
+            A.uu[d0 + j] = uj[j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 9; q++) S.Dinv[b][q] = Di[q];
+}
+
 // ------------------------------------------------------------------------- one cooperative substep
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
 template <typename T>
@@ -407,96 +531,20 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     __syncthreads();
     PHASE(2);
-    // ---- ABA pass 2 (leaves -> root): every lane computes the body update redundantly in registers
-    //      (no barriers); lane q publishes entry q of IA_parent / pA_parent, lane 0 the factorisation.
+    // ---- ABA pass 2 (leaves -> root) by tree level: 4 steps {shins, lower arms} -> {thighs, upper arms}
+    //      -> pelvis -> lwaist instead of 10 sequential bodies.  In a step, lane group g (4 lanes) updates
+    //      one body redundantly in registers (dof count padded to 3 with identity pivots, so every body runs
+    //      the same branch-free code), sums its own articulated inertia/bias force with its children's
+    //      contributions, and overwrites its IA/pA slots with its contribution to the parent (no longer
+    //      needed itself).  The base step below sums the torso with lwaist and both upper arms.
     auto& A = S.x.aba;
-#pragma unroll
-    for (int b = NB - 1; b >= 1; b--) {
-        const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
-        T IA[21], pAb[6], cb[6], Sc[3][6], U[3][6], D[9], Di[9], uj[3], W[3][6];
-#pragma unroll
-        for (int q = 0; q < 21; q++) IA[q] = A.IA[b][q];
-#pragma unroll
-        for (int e = 0; e < 6; e++) { pAb[e] = A.pA[b][e]; cb[e] = A.c[b][e]; }
-#pragma unroll
-        for (int j = 0; j < k; j++) {
-            const int d = d0 + j;
-            Sc[j][0] = S.u[d][0]; Sc[j][1] = S.u[d][1]; Sc[j][2] = S.u[d][2];
-            cross3(S.o[b], S.u[d], Sc[j] + 3);
-            symmv(IA, Sc[j], U[j]);
-            T sp = 0;
-#pragma unroll
-            for (int e = 0; e < 6; e++) sp += Sc[j][e] * pAb[e];
-            uj[j] = S.tau[d] - sp;
-            if (P.joint_damping) uj[j] -= M.damp[d] * S.nu[6 + d];
-        }
-#pragma unroll
-        for (int i = 0; i < k; i++) {
-#pragma unroll
-            for (int j = 0; j < k; j++) {
-                T t = 0;
-#pragma unroll
-                for (int e = 0; e < 6; e++) t += Sc[i][e] * U[j][e];
-                D[3 * i + j] = t;
-            }
-            if (P.joint_damping) D[4 * i] += dt * M.damp[d0 + i];
-        }
-        if (k == 1) small_inverse<T, 1>(D, Di);
-        else if (k == 2) small_inverse<T, 2>(D, Di);
-        else small_inverse<T, 3>(D, Di);
-#pragma unroll
-        for (int j = 0; j < k; j++)
-#pragma unroll
-            for (int e = 0; e < 6; e++) {
-                T t = 0;
-#pragma unroll
-                for (int i = 0; i < k; i++) t += U[i][e] * Di[3 * i + j];
-                W[j][e] = t;
-            }
-        // Ia = IA - W U^T (in place), pa = pA + Ia c + W u
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int cc = r; cc < 6; cc++) {
-                T t = IA[sidx(r, cc)];
-#pragma unroll
-                for (int j = 0; j < k; j++) t -= W[j][r] * U[j][cc];
-                IA[sidx(r, cc)] = t;
-            }
-        T pa[6];
-        symmv(IA, cb, pa);
-#pragma unroll
-        for (int e = 0; e < 6; e++) {
-            T t = pAb[e] + pa[e];
-#pragma unroll
-            for (int j = 0; j < k; j++) t += W[j][e] * uj[j];
-            pa[e] = t;
-        }
-        // publish: lane q -> IA_p[q] (and q+16), lanes 0..5 -> pA_p, lane 0 -> U, Dinv, uu
-        T v0 = 0, v1 = 0, v2 = 0;
-#pragma unroll
-        for (int q = 0; q < 21; q++) {
-            if (q == l) v0 = IA[q];
-            if (q == l + GL) v1 = IA[q];
-        }
-#pragma unroll
-        for (int e = 0; e < 6; e++)
-            if (e == l) v2 = pa[e];
-        A.IA[p][l] += v0;
-        if (l + GL < 21) A.IA[p][l + GL] += v1;
-        if (l < 6) A.pA[p][l] += v2;
-        if (l == 0) {
-#pragma unroll
-            for (int j = 0; j < k; j++) {
-#pragma unroll
-                for (int e = 0; e < 6; e++) S.U[d0 + j][e] = U[j][e];
-                A.uu[d0 + j] = uj[j];
-            }
-#pragma unroll
-            for (int q = 0; q < 9; q++) S.Dinv[b][q] = Di[q];
-        }
-        wave_sync();
-    }
+    group_aba_level<T, 0>(P, S, l >> 2, dt);
+    wave_sync();
+    group_aba_level<T, 1>(P, S, l >> 2, dt);
+    wave_sync();
+    group_aba_level<T, 2>(P, S, l >> 2, dt);
+    wave_sync();
+    group_aba_level<T, 3>(P, S, l >> 2, dt);
     __syncthreads();
     PHASE(3);
     // ---- base + pass 3 (redundant on every lane); lane 0 publishes L0 and nu* = clamp(nu + dt acc)
@@ -504,10 +552,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         T L[21], a[NB][6];
         T IA0[21];
 #pragma unroll
-        for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q];
+        for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q] + A.IA[1][q] + A.IA[7][q] + A.IA[9][q];   // torso + kids
         chol6(IA0, L);
 #pragma unroll
-        for (int e = 0; e < 6; e++) a[0][e] = -A.pA[0][e];
+        for (int e = 0; e < 6; e++) a[0][e] = -(A.pA[0][e] + A.pA[1][e] + A.pA[7][e] + A.pA[9][e]);
         chol6_solve(L, a[0]);
         T acc[NV];
 #pragma unroll
@@ -590,26 +638,72 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     __syncthreads();
     PHASE(5);
-    // ---- contacts: candidate c = 16*round + lane, compacted in candidate order
+    // ---- contacts, compacted in candidate order (ground points, then geom pairs)
     const int maxc = P.max_contacts < MAXC_G ? P.max_contacts : MAXC_G;
     int nc = 0, over = 0;
     const T basez = S.st[2];
-    for (int r0 = 0; r0 < NCAND; r0 += GL) {
+    const unsigned long long below16 = (lanemask_lt >> gbit) & 0xFFFFull;
+    auto emit = [&](bool hit, int ba, int bb, const T* pa, const T* pb, const T* n, T d) {
+        const unsigned long long bm = (__ballot(hit) >> gbit) & 0xFFFFull;
+        const int pos = nc + __popcll(bm & below16);
+        if (hit) {
+            if (pos < maxc) {
+                T* e = C.con[pos];
+                e[0] = (T)ba; e[1] = (T)bb;
+#pragma unroll
+                for (int i = 0; i < 3; i++) { e[2 + i] = pa[i]; e[5 + i] = pb[i]; e[8 + i] = n[i]; }
+                e[11] = d;
+            } else {
+                over = 1;
+            }
+        }
+        nc += __popcll(bm);
+    };
+    for (int r0 = 0; r0 < NCAND_GROUND; r0 += GL) {   // sphere / capsule end vs plane (cheap, exact)
         const int c = r0 + l;
         bool hit = false;
-        int ba = 0, bb = -1;
-        T pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
-        if (c < NCAND) {
-            const int ga = M.cand_a[c], gb = M.cand_b[c];
-            if (gb < 0) {   // ground point of geom ga, endpoint -1-gb
-                const int e = -1 - gb;
-                const T* p = C.gp[ga][e];
-                d = basez + p[2] - M.gr[ga];
-                hit = d < (T)P.contact_thresh;
-                ba = M.gbody[ga];
-                pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - M.gr[ga];
-                pb[0] = pa[0]; pb[1] = pa[1]; pb[2] = pa[2];
-            } else if (P.self_collision) {
+        int ba = 0;
+        T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
+        if (c < NCAND_GROUND) {
+            const int ga = M.cand_a[c], e = -1 - M.cand_b[c];
+            const T* p = C.gp[ga][e];
+            d = basez + p[2] - M.gr[ga];
+            hit = d < (T)P.contact_thresh;
+            ba = M.gbody[ga];
+            pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - M.gr[ga];
+        }
+        emit(hit, ba, -1, pa, pa, n, d);
+    }
+    if (P.self_collision) {
+        // broad phase: bounding spheres about the segment midpoints (conservative margin), survivors listed
+        // in pair order in the (not yet used) row storage; narrow phase (segment-segment) on survivors only
+        int* surv = reinterpret_cast<int*>(&C.row[MAXR_LDS - 3][0]);
+        const T reach = (T)P.contact_thresh + (T)1e-3;
+        int ns = 0;
+        for (int r0 = 0; r0 < NPAIR; r0 += GL) {
+            const int k = r0 + l;
+            bool maybe = false;
+            if (k < NPAIR) {
+                const int ga = M.cand_a[NCAND_GROUND + k], gb = M.cand_b[NCAND_GROUND + k];
+                T dm[3];
+#pragma unroll
+                for (int i = 0; i < 3; i++) dm[i] = (C.gp[ga][0][i] + C.gp[ga][1][i]) - (C.gp[gb][0][i] + C.gp[gb][1][i]);
+                const T rr = M.gbr[ga] + M.gbr[gb] + reach;
+                maybe = dot3(dm, dm) < T(4) * rr * rr;   // |ma - mb| < rr with ma = (p1 + p2) / 2
+            }
+            const unsigned long long bm = (__ballot(maybe) >> gbit) & 0xFFFFull;
+            if (maybe) surv[ns + __popcll(bm & below16)] = k;
+            ns += __popcll(bm);
+        }
+        wave_sync();
+        for (int r0 = 0; r0 < ns; r0 += GL) {
+            const int j = r0 + l;
+            bool hit = false;
+            int ba = 0, bb = -1;
+            T pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
+            if (j < ns) {
+                const int k = surv[j];
+                const int ga = M.cand_a[NCAND_GROUND + k], gb = M.cand_b[NCAND_GROUND + k];
                 T ca[3], cb[3], dv[3];
                 seg_seg(C.gp[ga][0], C.gp[ga][1], C.gp[gb][0], C.gp[gb][1], ca, cb);
 #pragma unroll
@@ -630,21 +724,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 ba = M.gbody[ga];
                 bb = M.gbody[gb];
             }
+            emit(hit, ba, bb, pa, pb, n, d);
         }
-        const unsigned long long bm = (__ballot(hit) >> gbit) & 0xFFFFull;
-        const int pos = nc + __popcll(bm & ((lanemask_lt >> gbit) & 0xFFFFull));
-        if (hit) {
-            if (pos < maxc) {
-                T* e = C.con[pos];
-                e[0] = (T)ba; e[1] = (T)bb;
-#pragma unroll
-                for (int i = 0; i < 3; i++) { e[2 + i] = pa[i]; e[5 + i] = pb[i]; e[8 + i] = n[i]; }
-                e[11] = d;
-            } else {
-                over = 1;
-            }
-        }
-        nc += __popcll(bm);
     }
     if (nc > maxc) { nc = maxc; over = 1; }
     if (over) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
@@ -671,6 +752,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             R[2 * NV + 3] = 0;
             R[2 * NV + 4] = T(1) / (sg * Mi[6 + d]);
             R[2 * NV + 5] = 0;
+            R[2 * NV + 6] = 0;
         } else {
             const int cidx = r < nl + nc ? r - nl : (r - nl - nc) >> 1;
             const int f = r < nl + nc ? 0 : 1 + ((r - nl - nc) & 1);
@@ -727,6 +809,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             R[2 * NV + 3] = 0;
             R[2 * NV + 4] = T(1) / jm;
             R[2 * NV + 5] = bb >= 0 ? (T)P.mu_self : (T)P.mu_ground;
+            R[2 * NV + 6] = 0;
         }
     }
     __syncthreads();
@@ -734,30 +817,99 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
     //      re-reads values it wrote itself, so no cross-lane LDS ordering is needed inside the loop.
     T n0 = S.nu[l], n1 = l < NV - GL ? S.nu[GL + l] : T(0);
-    auto lam_of = [&](int r) -> T { return r < MAXR_LDS ? C.row[r][2 * NV + 3] : grow[(r - MAXR_LDS) * RW + 2 * NV + 3]; };
-    auto solve = [&](T* R, int r) {
-        T lo = R[2 * NV + 1], hi = R[2 * NV + 2];
-        if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
-            const T mu = R[2 * NV + 5];
-            const T ln = lam_of(nl + ((r - nl - nc) >> 1));
-            lo = -mu * ln;
-            hi = mu * ln;
+    if (__ballot(nrows > MAXR_LDS) == 0) {
+        // Common case (every env of the wave keeps its rows in LDS): software-pipelined over the flattened
+        // (iteration, row) sequence - the next row's J / M^-1 J^T entries, scalars, lambda and (friction)
+        // normal lambda are read while the current row's 16-lane DPP reduction runs; the only values the
+        // current row can change for the next one (its own lambda when nrows == 1, or the normal lambda of
+        // the next friction row) are patched in registers.
+        struct RowRegs { T j0, j1, m0, m1, b, lo, hi, lam, meff, mu, ln; int nrm; };
+        // lanes without a second nu component read the row's zero pad: no branch or select on loaded values
+        const int lj1 = l < NV - GL ? GL + l : 2 * NV + 6, lm1 = l < NV - GL ? NV + GL + l : 2 * NV + 6;
+        auto load = [&](int r, RowRegs& d) {
+            const T* R = C.row[r];
+            d.j0 = R[l];
+            d.j1 = R[lj1];
+            d.m0 = R[NV + l];
+            d.m1 = R[lm1];
+            d.b = R[2 * NV + 0]; d.lo = R[2 * NV + 1]; d.hi = R[2 * NV + 2]; d.lam = R[2 * NV + 3];
+            d.meff = R[2 * NV + 4]; d.mu = R[2 * NV + 5];
+            d.nrm = r >= nl + nc ? nl + ((r - nl - nc) >> 1) : -1;   // friction row -> its normal row
+            d.ln = C.row[d.nrm >= 0 ? d.nrm : 0][2 * NV + 3];
+        };
+        // one Gauss-Seidel row update; `patch_*` substitute the lambda the previous row just produced for a
+        // value that was prefetched before it was written (its own lambda when nrows == 1, or the normal
+        // lambda of a friction row whose normal row was the previous one)
+        auto update = [&](RowRegs& d, int r, bool patch_lam, bool patch_ln, T prev) -> T {
+            if (patch_lam) d.lam = prev;
+            if (patch_ln) d.ln = prev;
+            T lo = d.lo, hi = d.hi;
+            if (d.nrm >= 0) {   // friction bounds from the normal impulse of the same contact
+                lo = -d.mu * d.ln;
+                hi = d.mu * d.ln;
+            }
+            const T part = d.j0 * n0 + d.j1 * n1;
+            const T jv = row_sum(part);
+            const T lnew = clampT(d.lam + d.meff * (d.b - jv), lo, hi);
+            C.row[r][2 * NV + 3] = lnew;
+            const T dl = lnew - d.lam;
+            n0 += d.m0 * dl;
+            n1 += d.m1 * dl;
+            return lnew;
+        };
+        const int total = P.iters * nrows;
+        if (total > 0) {
+            // ping-pong register sets A/B, loads issued unconditionally one row ahead (no phi copies that
+            // would force the loads to complete early)
+            RowRegs A, B;
+            load(0, A);
+            int r = 0;
+            bool pa_lam = false, pa_ln = false;
+            T prev = 0;
+            for (int k = 0;; k += 2) {
+                int rn = r + 1 == nrows ? 0 : r + 1;
+                load(rn, B);
+                bool pb_lam = rn == r, pb_ln = B.nrm == r;
+                prev = update(A, r, pa_lam, pa_ln, prev);
+                if (k + 1 >= total) break;
+                r = rn;
+                rn = r + 1 == nrows ? 0 : r + 1;
+                load(rn, A);
+                pa_lam = rn == r;
+                pa_ln = A.nrm == r;
+                prev = update(B, r, pb_lam, pb_ln, prev);
+                if (k + 2 >= total) break;
+                r = rn;
+            }
         }
-        const T part = R[l] * n0 + (l < NV - GL ? R[GL + l] * n1 : T(0));
-        const T m0 = R[NV + l], m1 = l < NV - GL ? R[NV + GL + l] : T(0);
-        const T jv = row_sum(part);
-        const T lam = R[2 * NV + 3];
-        const T lnew = clampT(lam + R[2 * NV + 4] * (R[2 * NV + 0] - jv), lo, hi);
-        const T dl = lnew - lam;
-        R[2 * NV + 3] = lnew;
-        n0 += m0 * dl;
-        n1 += m1 * dl;
-    };
-    for (int it = 0; it < P.iters; it++) {
-        const int nr_lds = nrows < MAXR_LDS ? nrows : MAXR_LDS;
-        for (int r = 0; r < nr_lds; r++) solve(C.row[r], r);
-        for (int r = MAXR_LDS; r < nrows; r++) solve(grow + (r - MAXR_LDS) * RW, r);
+    } else {
+        // some env spilled rows to its global region: plain loop with separately typed LDS / global rows
+        auto lam_of = [&](int r) -> T { return r < MAXR_LDS ? C.row[r][2 * NV + 3] : grow[(r - MAXR_LDS) * RW + 2 * NV + 3]; };
+        auto solve = [&](T* R, int r) {
+            T lo = R[2 * NV + 1], hi = R[2 * NV + 2];
+            if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
+                const T mu = R[2 * NV + 5];
+                const T ln = lam_of(nl + ((r - nl - nc) >> 1));
+                lo = -mu * ln;
+                hi = mu * ln;
+            }
+            const T part = R[l] * n0 + (l < NV - GL ? R[GL + l] * n1 : T(0));
+            const T m0 = R[NV + l], m1 = l < NV - GL ? R[NV + GL + l] : T(0);
+            const T jv = row_sum(part);
+            const T lam = R[2 * NV + 3];
+            const T lnew = clampT(lam + R[2 * NV + 4] * (R[2 * NV + 0] - jv), lo, hi);
+            const T dl = lnew - lam;
+            R[2 * NV + 3] = lnew;
+            n0 += m0 * dl;
+            n1 += m1 * dl;
+        };
+        for (int it = 0; it < P.iters; it++) {
+            const int nr_lds = nrows < MAXR_LDS ? nrows : MAXR_LDS;
+            for (int r = 0; r < nr_lds; r++) solve(C.row[r], r);
+            for (int r = MAXR_LDS; r < nrows; r++) solve(grow + (r - MAXR_LDS) * RW, r);
+        }
     }
+    PHASE(8);
     S.nu[l] = n0;
     if (l < NV - GL) S.nu[GL + l] = n1;
     // ---- integrate (lanes split the state), lane 0 the quaternion
