@@ -614,7 +614,7 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++)
-            group_substep(a.P, S, (T*)a.scratch + (long)(valid ? i : 0) * GROW_PER_ENV, l, ef);
+            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * EPB_ * GROW_PER_ENV, l, ef);
     }
     PHASE_INIT;
     if (valid && l == 0) {
@@ -847,7 +847,8 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (st == hipSuccess) st = hipMalloc((void**)&e->d.bi, NBOOK_I * n * sizeof(int));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d.bd, NBOOK_D * n * sizeof(double));
     if (st == hipSuccess)   // per-lane rows (kernel 0) or the per-env row spill region (kernel 1)
-        st = hipMalloc(&e->d.scratch, (size_t)(cfg->kernel == 1 ? GROW_PER_ENV : SCRATCH_PER_LANE) * n * e->real_size);
+        // (cooperative kernel: per-block regions, so round the lane count up to a multiple of 4 envs)
+        st = hipMalloc(&e->d.scratch, (size_t)(cfg->kernel == 1 ? GROW_PER_ENV * ((n + 3) / 4 * 4) : SCRATCH_PER_LANE * n) * e->real_size);
     if (st == hipSuccess) st = hipMalloc((void**)&e->eflags, sizeof(unsigned));
     if (st == hipSuccess) st = hipMalloc((void**)&e->clips_dev, HUM_MAX_CLIPS * sizeof(ClipDev));
     if (st == hipSuccess) st = hipMemset(e->clips_dev, 0, HUM_MAX_CLIPS * sizeof(ClipDev));

@@ -286,6 +286,135 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
     }
 }
 
+// ------------------------------------------------------------------------- constraint rows, wave-wide
+// Row t of the wave's concatenated row list (env 0's rows, then env 1's, ...) goes to lane t % (16 EPB_):
+// per-env counts are wave-uniform (readlane), so the env/row of a task is two compares away.
+template <typename T>
+__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc) {
+#pragma unroll
+    for (int q = 0; q < NV; q++) { R[q] = J[q]; R[NV + q] = Mi[q]; }
+#pragma unroll
+    for (int q = 0; q < 7; q++) R[2 * NV + q] = sc[q];
+}
+template <typename T>
+__device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J, const T* Mi, const T* sc) {
+    // spilled rows: nontemporal stores keep the compiler from merging this path with the LDS one into
+    // generic (flat) stores
+#pragma unroll
+    for (int q = 0; q < NV; q++) { __builtin_nontemporal_store(J[q], R + q); __builtin_nontemporal_store(Mi[q], R + NV + q); }
+#pragma unroll
+    for (int q = 0; q < 7; q++) __builtin_nontemporal_store(sc[q], R + 2 * NV + q);
+}
+
+template <typename T, int EPB_>
+__device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, GroupLDS<T>* shb, T* grow_block, int nl, int nc,
+                                                          const T dt) {
+    const ModelTab<T>& M = tab<T>();
+    const int lane = threadIdx.x & 63;
+    int cnt[EPB_], nls[EPB_], ncs[EPB_], pre[EPB_ + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) {
+        nls[e] = __builtin_amdgcn_readlane(nl, e * GL);
+        ncs[e] = __builtin_amdgcn_readlane(nc, e * GL);
+        cnt[e] = nls[e] + 3 * ncs[e];
+        pre[e + 1] = pre[e] + cnt[e];
+    }
+    const int total = pre[EPB_];
+    for (int t = lane; t < total; t += EPB_ * GL) {
+        int e = 0;
+#pragma unroll
+        for (int q = 1; q < EPB_; q++) e += t >= pre[q] ? 1 : 0;
+        int r = t, enl = nls[0], enc = ncs[0];
+#pragma unroll
+        for (int q = 0; q < EPB_; q++)
+            if (q == e) { r = t - pre[q]; enl = nls[q]; enc = ncs[q]; }
+        const GroupLDS<T>& S = shb[e];
+        const auto& C = S.x.cr;
+        T J[NV], Mi[NV], sc[7];
+#pragma unroll
+        for (int q = 0; q < NV; q++) J[q] = 0;
+        if (r < enl) {
+            const int d = C.rdesc[r] & 0xff, side = C.rdesc[r] >> 8;
+            const T sg = side == 0 ? T(1) : T(-1);
+            const T q = S.st[13 + d];
+            const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
+            g_response(S, -1, (const T*)nullptr, -1, (const T*)nullptr, d, sg, Mi);
+#pragma unroll
+            for (int k = 0; k < NV; k++) J[k] = (k == 6 + d) ? sg : T(0);
+            T mdd = 0;
+#pragma unroll
+            for (int k = 0; k < NDOF; k++) if (k == d) mdd = Mi[6 + k];
+            sc[0] = -pen * (T)P.erp_limit / dt;
+            sc[1] = 0;
+            sc[2] = (T)P.limit_max_impulse;
+            sc[3] = 0;
+            sc[4] = T(1) / (sg * mdd);
+            sc[5] = 0;
+            sc[6] = 0;
+        } else {
+            const int cidx = r < enl + enc ? r - enl : (r - enl - enc) >> 1;
+            const int f = r < enl + enc ? 0 : 1 + ((r - enl - enc) & 1);
+            const T* ce = C.con[cidx];
+            const int ba = (int)ce[0], bb = (int)ce[1];
+            const T pa[3] = {ce[2], ce[3], ce[4]}, pb[3] = {ce[5], ce[6], ce[7]}, n[3] = {ce[8], ce[9], ce[10]};
+            const T d = ce[11];
+            T dir[3];
+            if (f == 0) {
+                dir[0] = n[0]; dir[1] = n[1]; dir[2] = n[2];
+            } else {
+                T Va[6], Vb[6], va[3], vb[3] = {0, 0, 0}, vr[3];
+                g_body_vel(S, ba, Va);
+                cross3(Va, pa, va);
+#pragma unroll
+                for (int i = 0; i < 3; i++) va[i] += Va[3 + i];
+                if (bb >= 0) {
+                    g_body_vel(S, bb, Vb);
+                    cross3(Vb, pb, vb);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) vb[i] += Vb[3 + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 3; i++) vr[i] = va[i] - vb[i];
+                const T vn = dot3(vr, n);
+                T lat[3], t1[3], t2[3];
+#pragma unroll
+                for (int i = 0; i < 3; i++) lat[i] = vr[i] - n[i] * vn;
+                const T l2 = dot3(lat, lat);
+                if (l2 > (T)1e-12) {
+                    const T il = T(1) / sqrt(l2);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
+                    cross3(t1, n, t2);
+                } else {
+                    plane_space(n, t1, t2);
+                }
+#pragma unroll
+                for (int i = 0; i < 3; i++) dir[i] = f == 1 ? t1[i] : t2[i];
+            }
+            T fa[6], fb[6];
+            cross3(pa, dir, fa); fa[3] = dir[0]; fa[4] = dir[1]; fa[5] = dir[2];
+            cross3(pb, dir, fb);
+            fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
+            g_row_jacobian(S, ba, fa, T(1), J);
+            if (bb >= 0) g_row_jacobian(S, bb, fb, T(1), J);
+            g_response(S, ba, fa, bb, fb, -1, T(0), Mi);
+            T jm = 0;
+#pragma unroll
+            for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];
+            sc[0] = f == 0 ? (d > 0 ? -d / dt : -d * (T)P.erp_contact / dt) : T(0);
+            sc[1] = 0;
+            sc[2] = (T)1e10;
+            sc[3] = 0;
+            sc[4] = T(1) / jm;
+            sc[5] = bb >= 0 ? (T)P.mu_self : (T)P.mu_ground;
+            sc[6] = 0;
+        }
+        if (r < MAXR_LDS) store_row(shb[e].x.cr.row[r], J, Mi, sc);
+        else store_row_global(grow_block + (long)e * GROW_PER_ENV + (r - MAXR_LDS) * RW, J, Mi, sc);
+    }
+}
+
 // ------------------------------------------------------------------------- ABA pass 2, one tree level
 // Level tables (body per 4-lane group): children are always processed in an earlier level.
 constexpr int LVL_BODY[4][4] = {{4, 6, 8, 10}, {3, 5, 7, 9}, {2, 2, 2, 2}, {1, 1, 1, 1}};
@@ -400,8 +529,11 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 
 // ------------------------------------------------------------------------- one cooperative substep
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
-template <typename T>
-__device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>& S, T* grow, const int l, unsigned& ef) {
+template <typename T, int EPB_>
+__device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>* shb, const int ge,
+                                                             T* grow_block, const int l, unsigned& ef) {
+    GroupLDS<T>& S = shb[ge];
+    T* grow = grow_block + (long)ge * GROW_PER_ENV;
     const ModelTab<T>& M = tab<T>();
     const T dt = (T)P.dt;
     PHASE_INIT;
@@ -731,87 +863,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     if (over) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
     __syncthreads();
     PHASE(6);
-    // ---- rows: one per lane (limits, normals, frictions), Jacobian + response
+    // ---- rows (limits, normals, frictions): Jacobian + test-impulse response, one row per lane, the rows of
+    //      all EPB_ envs of the wave spread over its lanes (one round instead of max_e ceil(nrows_e / 16))
     const int nrows = nl + 3 * nc;
-    for (int r = l; r < nrows; r += GL) {
-        T J[NV], Mi[NV];
-#pragma unroll
-        for (int e = 0; e < NV; e++) J[e] = 0;
-        T* R = r < MAXR_LDS ? C.row[r] : grow + (r - MAXR_LDS) * RW;
-        if (r < nl) {
-            const int d = C.rdesc[r] & 0xff, side = C.rdesc[r] >> 8;
-            const T sg = side == 0 ? T(1) : T(-1);
-            const T q = S.st[13 + d];
-            const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
-            g_response(S, -1, (const T*)nullptr, -1, (const T*)nullptr, d, sg, Mi);
-#pragma unroll
-            for (int e = 0; e < NV; e++) { R[e] = (e == 6 + d) ? sg : T(0); R[NV + e] = Mi[e]; }
-            R[2 * NV + 0] = -pen * (T)P.erp_limit / dt;
-            R[2 * NV + 1] = 0;
-            R[2 * NV + 2] = (T)P.limit_max_impulse;
-            R[2 * NV + 3] = 0;
-            R[2 * NV + 4] = T(1) / (sg * Mi[6 + d]);
-            R[2 * NV + 5] = 0;
-            R[2 * NV + 6] = 0;
-        } else {
-            const int cidx = r < nl + nc ? r - nl : (r - nl - nc) >> 1;
-            const int f = r < nl + nc ? 0 : 1 + ((r - nl - nc) & 1);
-            const T* e = C.con[cidx];
-            const int ba = (int)e[0], bb = (int)e[1];
-            const T pa[3] = {e[2], e[3], e[4]}, pb[3] = {e[5], e[6], e[7]}, n[3] = {e[8], e[9], e[10]};
-            const T d = e[11];
-            T dir[3];
-            if (f == 0) {
-                dir[0] = n[0]; dir[1] = n[1]; dir[2] = n[2];
-            } else {
-                T Va[6], Vb[6], va[3], vb[3] = {0, 0, 0}, vr[3];
-                g_body_vel(S, ba, Va);
-                cross3(Va, pa, va);
-#pragma unroll
-                for (int i = 0; i < 3; i++) va[i] += Va[3 + i];
-                if (bb >= 0) {
-                    g_body_vel(S, bb, Vb);
-                    cross3(Vb, pb, vb);
-#pragma unroll
-                    for (int i = 0; i < 3; i++) vb[i] += Vb[3 + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 3; i++) vr[i] = va[i] - vb[i];
-                const T vn = dot3(vr, n);
-                T lat[3], t1[3], t2[3];
-#pragma unroll
-                for (int i = 0; i < 3; i++) lat[i] = vr[i] - n[i] * vn;
-                const T l2 = dot3(lat, lat);
-                if (l2 > (T)1e-12) {
-                    const T il = T(1) / sqrt(l2);
-#pragma unroll
-                    for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
-                    cross3(t1, n, t2);
-                } else {
-                    plane_space(n, t1, t2);
-                }
-#pragma unroll
-                for (int i = 0; i < 3; i++) dir[i] = f == 1 ? t1[i] : t2[i];
-            }
-            T fa[6], fb[6];
-            cross3(pa, dir, fa); fa[3] = dir[0]; fa[4] = dir[1]; fa[5] = dir[2];
-            cross3(pb, dir, fb);
-            fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
-            g_row_jacobian(S, ba, fa, T(1), J);
-            if (bb >= 0) g_row_jacobian(S, bb, fb, T(1), J);
-            g_response(S, ba, fa, bb, fb, -1, T(0), Mi);
-            T jm = 0;
-#pragma unroll
-            for (int q = 0; q < NV; q++) { R[q] = J[q]; R[NV + q] = Mi[q]; jm += J[q] * Mi[q]; }
-            R[2 * NV + 0] = f == 0 ? (d > 0 ? -d / dt : -d * (T)P.erp_contact / dt) : T(0);
-            R[2 * NV + 1] = 0;
-            R[2 * NV + 2] = (T)1e10;
-            R[2 * NV + 3] = 0;
-            R[2 * NV + 4] = T(1) / jm;
-            R[2 * NV + 5] = bb >= 0 ? (T)P.mu_self : (T)P.mu_ground;
-            R[2 * NV + 6] = 0;
-        }
-    }
+    group_rows<T, EPB_>(P, shb, grow_block, nl, nc, dt);
     __syncthreads();
     PHASE(7);
     // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
