@@ -1,0 +1,713 @@
+// kernels.h - device side of the vectorised humanoid env: SoA lane I/O, LowLevelHumanoidEnv and
+// HierarchicalHumanoidEnv logic (reset / post-physics step), and the step / reset / aux kernels.
+//
+// Shared by two translation units: humanoid_env.hip (C-ABI host code + every kernel variant except the
+// benchmarked one) and group_f32.hip, which instantiates ONLY step_group_kernel<float, 4>.  Compiling the
+// hot kernel alone keeps its code generation independent of its sibling variants (co-compiled template
+// variants share inlining and register-allocation decisions: measured 0.294 vs 0.250 ms per step).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/humanoid_env.h"
+#include "physics.h"
+#include "envlogic.h"
+#include "physics_group.h"
+
+namespace hkk {
+using namespace hk;
+
+constexpr int NBOOK_I = 11;   // frame, timestep, pred_idx, clip, rng_ctr, mode, rng key lo, rng key hi
+                              // | hier: level_rem, n_high, expect_high
+constexpr int NBOOK_D = 30;   // target3 srp3 robot_pos3 sep3 hldt wt2 lts dj dvj bps es jls alive dlts
+                              // | hier: hts cum_drift drift dhts cum_alive bxy2
+
+struct DevState {
+    void* phys;        // Real [47][n]
+    int* bi;           // [6][n]
+    double* bd;        // [23][n]
+    void* scratch;     // Real [SCRATCH_PER_LANE][n]
+    float* aux_tmp;
+};
+
+struct KArgs {
+    int n;
+    unsigned long long seed;
+    long long lane_offset;
+    PhysParams P;
+    const ClipDev* clips;   // device array [HUM_MAX_CLIPS] (a by-value array here is dynamically indexed -> scratch copy)
+    const double* pred;
+    int npred;
+    void* phys;
+    int* bi;
+    double* bd;
+    void* scratch;
+    unsigned* eflags;
+    // step
+    const float* act;
+    float* obs;
+    float* rew;
+    unsigned char* done;
+    int* frame_out;
+    float* obs_reset;
+    unsigned flags;
+    // reset
+    const unsigned char* mask;
+    const int* start_frame;
+    const double* reset_yaw;
+    float* aux;
+    // hierarchical env (hum_hier_step / hum_hier_reset)
+    int hier;
+    const float* act_high;          // [n,2]
+    const unsigned char* agent_sel; // [n] 1 = high, 0 = low (NULL = the lane's expected agent)
+    unsigned char* agents;          // [n] HUM_AGENT_* present in the returned dicts
+    float* obs_high;                // [n,44]
+    float* rew_high;                // [n]
+    float* obs_high_reset;          // [n,44]
+};
+
+// ----------------------------------------------------------------------------------- SoA lane I/O
+__device__ inline void load_book(const KArgs& a, int i, Book& b) {
+    const int* bi = a.bi;
+    b.frame = bi[0 * a.n + i]; b.timestep = bi[1 * a.n + i]; b.pred_idx = bi[2 * a.n + i];
+    b.clip = bi[3 * a.n + i]; b.rng_ctr = (unsigned)bi[4 * a.n + i]; b.mode = (unsigned)bi[5 * a.n + i];
+    b.rng_key = (unsigned long long)(unsigned)bi[6 * a.n + i] | ((unsigned long long)(unsigned)bi[7 * a.n + i] << 32);
+    const double* d = a.bd;
+    auto D = [&](int e) { return d[(long)e * a.n + i]; };
+    for (int k = 0; k < 3; k++) { b.target[k] = D(k); b.srp[k] = D(3 + k); b.robot_pos[k] = D(6 + k); b.sep[k] = D(9 + k); }
+    b.hldt = D(12); b.wt[0] = D(13); b.wt[1] = D(14); b.lts = D(15);
+    b.dj = D(16); b.dvj = D(17); b.bps = D(18); b.es = D(19); b.jls = D(20); b.alive = D(21); b.dlts = D(22);
+    if (a.hier) {
+        b.level_rem = bi[8 * a.n + i]; b.n_high = bi[9 * a.n + i]; b.expect_high = bi[10 * a.n + i];
+        b.hts = D(23); b.cum_drift = D(24); b.drift = D(25); b.dhts = D(26); b.cum_alive = D(27);
+        b.bxy[0] = D(28); b.bxy[1] = D(29);
+    }
+}
+template <typename T>
+__device__ inline void load_lane(const KArgs& a, int i, T* st, Book& b) {
+    const T* ph = (const T*)a.phys;
+#pragma unroll
+    for (int e = 0; e < HUM_NSTATE; e++) st[e] = ph[(long)e * a.n + i];
+    load_book(a, i, b);
+}
+__device__ inline void store_book(const KArgs& a, int i, const Book& b) {
+    int* bi = a.bi;
+    bi[0 * a.n + i] = b.frame; bi[1 * a.n + i] = b.timestep; bi[2 * a.n + i] = b.pred_idx;
+    bi[3 * a.n + i] = b.clip; bi[4 * a.n + i] = (int)b.rng_ctr; bi[5 * a.n + i] = (int)b.mode;
+    double* d = a.bd;
+    auto D = [&](int e) -> double& { return d[(long)e * a.n + i]; };
+    for (int k = 0; k < 3; k++) { D(k) = b.target[k]; D(3 + k) = b.srp[k]; D(6 + k) = b.robot_pos[k]; D(9 + k) = b.sep[k]; }
+    D(12) = b.hldt; D(13) = b.wt[0]; D(14) = b.wt[1]; D(15) = b.lts;
+    D(16) = b.dj; D(17) = b.dvj; D(18) = b.bps; D(19) = b.es; D(20) = b.jls; D(21) = b.alive; D(22) = b.dlts;
+    if (a.hier) {
+        bi[8 * a.n + i] = b.level_rem; bi[9 * a.n + i] = b.n_high; bi[10 * a.n + i] = b.expect_high;
+        D(23) = b.hts; D(24) = b.cum_drift; D(25) = b.drift; D(26) = b.dhts; D(27) = b.cum_alive;
+        D(28) = b.bxy[0]; D(29) = b.bxy[1];
+    }
+}
+template <typename T>
+__device__ inline void store_lane(const KArgs& a, int i, const T* st, const Book& b) {
+    T* ph = (T*)a.phys;
+#pragma unroll
+    for (int e = 0; e < HUM_NSTATE; e++) ph[(long)e * a.n + i] = st[e];
+    store_book(a, i, b);
+}
+
+__device__ inline int draw(const KArgs& a, int i, Book& b, int lo, int hi) {
+    return lane_draw_key(b.rng_key, b.rng_ctr++, lo, hi);
+}
+
+// ----------------------------------------------------------------------------------- reset
+// LowLevelHumanoidEnv.reset() / resetFromFrame() (low_level_env.py:224-305)
+template <typename T>
+__device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* obs,
+                           unsigned& ef) {
+    const ClipDev& c = a.clips[b.clip];
+    if (start_frame < 0) start_frame = draw(a, i, b, 0, c.max_frame - 5);   // :228
+    // flat_env.reset(): restoreState -> zero velocities (all 17 joints overwritten below)
+#pragma unroll
+    for (int e = 0; e < HUM_NSTATE; e++) st[e] = 0;
+    st[6] = 1;
+    b.timestep = 0;
+    if ((b.mode & HUM_MODE_PREDEFINED) && a.npred > 0) {                   // :253-255
+        b.pred_idx = 0;
+        for (int k = 0; k < 3; k++) b.target[k] = a.pred[k];
+    } else {                                                                // :257, getRandomVec :240-245
+        const double r = 0 + (double)draw(a, i, b, -180, 180) * DEG2RAD;
+        b.target[0] = cos(r) * 5;
+        b.target[1] = sin(r) * 5;
+        b.target[2] = 0;
+    }
+    b.frame = start_frame;                                                  // :259-261 setJointsOrientation
+    int vrow = start_frame;
+    if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
+#pragma unroll
+    for (int j = 0; j < NREF; j++) {
+        st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
+        st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+    }
+    for (int k = 0; k < 3; k++) { b.robot_pos[k] = 0; b.srp[k] = 0; }      // :264-268
+    st[0] = 0; st[1] = 0; st[2] = (T)1.17;
+    const double degToTarget = atan2(b.target[1], b.target[0]) * RAD2DEG;  // :270
+    b.wt[0] = cos(degToTarget) * 1000;                                      // :271 (degrees into cos: quirk)
+    b.wt[1] = sin(degToTarget) * 1000;
+    const double th = (degToTarget + reset_yaw) * DEG2RAD;                  // :272-273 scipy from_euler
+    st[3] = 0; st[4] = 0; st[5] = (T)sin(th / 2); st[6] = (T)cos(th / 2);
+    b.hldt = degToTarget * DEG2RAD;                                         // :275
+    // starting_ep_pos (:277-289) and the initial base velocity (:291-295)
+    const int f0 = b.frame, f1 = (b.frame + 2) % c.max_frame;
+    const double phi = degToTarget * DEG2RAD;
+    const double qz = sin(phi / 2), qw = cos(phi / 2);
+    const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
+    {
+        Kin<T> K;
+        forward_kinematics(st + 3, st + 13, K);
+        T pp[NPART][3];
+        part_positions(K, pp);
+        const double rfx = (double)st[0] + (double)pp[PART_RIGHT_FOOT][0];
+        const double rfy = (double)st[1] + (double)pp[PART_RIGHT_FOOT][1];
+        const double* e0 = c.ep + f0 * 27;
+        const double* e1 = c.ep + f1 * 27;
+        const double refx = r00 * e0[EP_RIGHT_FOOT] + r01 * e0[EP_RIGHT_FOOT + 1];
+        const double refy = r10 * e0[EP_RIGHT_FOOT] + r11 * e0[EP_RIGHT_FOOT + 1];
+        b.sep[0] = rfx - refx; b.sep[1] = rfy - refy; b.sep[2] = 0;
+        const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
+        const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
+        st[7] = (T)(((l1x - l0x) / 0.0165) / 1.2);
+        st[8] = (T)(((l1y - l0y) / 0.0165) / 1.2);
+        st[9] = (T)(((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165) / 1.2);
+    }
+    b.lts = 0; b.dj = 0; b.dvj = 0; b.bps = 0; b.es = 0; b.jls = 0; b.alive = 0; b.dlts = 0;   // initReward
+    inc_frame(b, c, 2);                                                     // :302
+    float js[NDOF];
+    int jal;
+    PostPhys<T> pp;
+    calc_state(st, b.wt, obs, js, jal, pp);                                 // :304-305
+    ref_obs(c, b.frame, obs + 42, ef);
+}
+
+// Post-physics part of step (low_level_env.py:481-526) + optional auto-reset; stores state, book, outputs.
+template <typename T>
+__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef) {
+    const ClipDev& c = a.clips[b.clip];
+    float obs[HUM_NOBS];
+    // calc_state (:481) and robot_pos (:483-486)
+    float js[NDOF];
+    int jal;
+    PostPhys<T> pp;
+    calc_state(st, b.wt, obs, js, jal, pp);
+    b.robot_pos[0] = pp.bx; b.robot_pos[1] = pp.by; b.robot_pos[2] = 0;
+    // updateReward (:441-465)
+    double dJ = 0, dV = 0;
+#pragma unroll
+    for (int j = 0; j < NREF; j++) {
+        dJ = dJ + fabs(pp.q[JM_DOF[j]] - c.pos[b.frame * 14 + JM_COL[j]]) * JM_W[j];
+    }
+    int vrow = b.frame;
+    if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
+#pragma unroll
+    for (int j = 0; j < NREF; j++) {
+        dV = dV + fabs(pp.qd[JM_DOF[j]] - c.vel[vrow * 14 + JM_COL[j]]) * JM_WV[j];
+    }
+    const double jointScore = exp(4 * (-dJ / JOINT_WEIGHT_SUM));
+    const double jointVelScore = exp((-dV / JOINT_VEL_WEIGHT_SUM) / 2);
+    const double lowTarget = -norm3_blas(b.target[0] - b.robot_pos[0], b.target[1] - b.robot_pos[1], b.target[2] - b.robot_pos[2]);
+    const double posture = exp(-((fabs(pp.yaw - b.hldt) + fabs(pp.roll)) + fabs(pp.pitch)));
+    b.dlts = (lowTarget - b.lts) / 0.0165 * 0.1;
+    b.dj = jointScore;
+    b.dvj = jointVelScore;
+    b.lts = lowTarget;
+    {
+        const float run = pairwise_sum_f<HUM_NACT>([&](int k) { return fabsf(act[k] * js[k]); }) / 17.0f;
+        const float stall = pairwise_sum_f<HUM_NACT>([&](int k) { return act[k] * act[k]; }) / 17.0f;
+        b.es = -1.0 * (double)run + -0.1 * (double)stall;
+    }
+    b.jls = -0.1 * jal;
+    b.alive = ((obs[0] + 0.8f) > 0.75f) ? 2.0 : -1.0;
+    b.bps = posture;
+    double total = 0;
+    total = total + b.dj * REWARD_W[0];
+    total = total + b.dvj * REWARD_W[1];
+    total = total + b.dlts * REWARD_W[2];
+    total = total + b.es * REWARD_W[3];
+    total = total + b.jls * REWARD_W[4];
+    total = total + b.alive * REWARD_W[5];
+    total = total + b.bps * REWARD_W[6];
+    inc_frame(b, c, 2);                                                      // :513
+    // checkTarget (:412-434)
+    {
+        const double dist = norm3_blas(b.robot_pos[0] - b.target[0], b.robot_pos[1] - b.target[1], b.robot_pos[2] - b.target[2]);
+        if (dist <= 0.5) {
+            const double rr = pp.yaw + (double)draw(a, i, b, -180, 180) * DEG2RAD;
+            double nt[3] = {b.robot_pos[0] + cos(rr) * 5, b.robot_pos[1] + sin(rr) * 5, b.robot_pos[2] + 0.0};
+            if ((b.mode & HUM_MODE_PREDEFINED) && a.npred > 0) {
+                b.pred_idx = (b.pred_idx + 1) % a.npred;
+                for (int k = 0; k < 3; k++) nt[k] = a.pred[3 * b.pred_idx + k];
+            }
+            for (int k = 0; k < 3; k++) { b.srp[k] = b.target[k]; b.target[k] = nt[k]; }
+            b.lts = -norm3_blas(b.target[0] - b.srp[0], b.target[1] - b.srp[1], b.target[2] - b.srp[2]);
+        }
+        set_walk_target_hl(b);
+    }
+    ref_obs(c, b.frame, obs + 42, ef);                                        // :519
+    bool done;                                                                // :521-524
+    {
+        const bool alive = b.alive > 0;
+        const bool near = norm3_blas(b.target[0] - b.robot_pos[0], b.target[1] - b.robot_pos[1], b.target[2] - b.robot_pos[2]) <=
+                          norm3_blas(b.target[0] - b.srp[0], b.target[1] - b.srp[1], b.target[2] - b.srp[2]) + 3;
+        done = (b.mode & HUM_MODE_DEBUG) ? !alive : !(alive && near);
+        b.timestep += 1;
+        if (b.timestep >= 3000) done = true;
+    }
+#pragma unroll
+    for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = obs[k];
+    a.rew[i] = (float)total;
+    a.done[i] = done ? 1 : 0;
+    if (a.frame_out) a.frame_out[i] = b.frame;
+    if (done && (a.flags & HUM_STEP_AUTORESET)) {
+        float o2[HUM_NOBS];
+        reset_lane(a, i, st, b, -1, 0.0, o2, ef);
+        if (a.obs_reset) {
+#pragma unroll
+            for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[(long)i * HUM_NOBS + k] = o2[k];
+        }
+    }
+    store_lane(a, i, st, b);
+    if (ef) atomicOr(a.eflags, ef);
+}
+
+
+// ----------------------------------------------------------------------------------- hierarchical env
+// HierarchicalHumanoidEnv (/root/reference/hier_env.py) on the same lanes/physics.  float64 in the reference's
+// operation order; contraction off (numpy never fuses a*b+c); 3-vector norms/dots in OpenBLAS ddot order.
+#pragma clang fp contract(off)
+
+// getHighLevelObs (hier_env.py:336-353): [obs0, cos/sin(angle to target), cos/sin(angle to start), obs3..41]
+__device__ inline void hier_high_obs(const float* obs42, const Book& b, double yaw, float* o44) {
+    const double targetTheta = atan2(b.target[1] - b.robot_pos[1], b.target[0] - b.robot_pos[0]);
+    const double angleToTarget = targetTheta - yaw;
+    const double startPosTheta = atan2(b.srp[1] - b.robot_pos[1], b.srp[0] - b.robot_pos[0]);
+    const double angleToStart = startPosTheta - yaw;
+    o44[0] = obs42[0];
+    o44[1] = (float)cos(angleToTarget);
+    o44[2] = (float)sin(angleToTarget);
+    o44[3] = (float)cos(angleToStart);
+    o44[4] = (float)sin(angleToStart);
+#pragma unroll
+    for (int k = 3; k < 42; k++) o44[k + 2] = obs42[k];
+}
+
+// reset() / resetFromFrame() (hier_env.py:235-319)
+template <typename T>
+__device__ void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* o44,
+                                unsigned& ef) {
+    const ClipDev& c = a.clips[b.clip];
+    if (start_frame < 0) {                                                  // :238-241 (argument order)
+        start_frame = draw(a, i, b, 0, c.max_frame - 5);
+        reset_yaw = (double)draw(a, i, b, -180, 180);
+    }
+#pragma unroll
+    for (int e = 0; e < HUM_NSTATE; e++) st[e] = 0;                         // flat_env.reset()
+    st[6] = 1;
+    b.timestep = 0;
+    if ((b.mode & HUM_MODE_PREDEFINED) && a.npred > 0) {                   // :264-266
+        b.pred_idx = 0;
+        for (int k = 0; k < 3; k++) b.target[k] = a.pred[k];
+    } else {                                                                // :268, getRandomVec :251-257
+        const double r = 0 + (double)draw(a, i, b, -180, 180) * DEG2RAD;
+        b.target[0] = cos(r) * 5;
+        b.target[1] = sin(r) * 5;
+        b.target[2] = 0;
+    }
+    b.frame = start_frame;                                                  // :272-274 setJointsOrientation
+    int vrow = start_frame;
+    if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
+#pragma unroll
+    for (int j = 0; j < NREF; j++) {
+        st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
+        st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+    }
+    for (int k = 0; k < 3; k++) { b.robot_pos[k] = 0; b.srp[k] = 0; }      // :277-281
+    st[0] = 0; st[1] = 0; st[2] = (T)1.17;
+    const double degToTarget = atan2(b.target[1], b.target[0]) * RAD2DEG + reset_yaw;   // :284
+    b.wt[0] = cos(degToTarget) * 1000;                                      // :285 (degrees into cos: quirk)
+    b.wt[1] = sin(degToTarget) * 1000;
+    const double th = degToTarget * DEG2RAD;                                // :286-287 scipy from_euler
+    st[3] = 0; st[4] = 0; st[5] = (T)sin(th / 2); st[6] = (T)cos(th / 2);
+    b.hldt = degToTarget * DEG2RAD;                                         // :289
+    {                                                                       // :291-304 starting velocity
+        const int f0 = b.frame, f1 = b.frame + 1;
+        const double qz = sin(th / 2), qw = cos(th / 2);
+        const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
+        const double* e0 = c.ep + f0 * 27;
+        const double* e1 = c.ep + f1 * 27;
+        const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
+        const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
+        st[7] = (T)((l1x - l0x) / 0.0165);
+        st[8] = (T)((l1y - l0y) / 0.0165);
+        st[9] = (T)((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165);
+    }
+    // initReward (:183-206); starting_ep_pos is NOT reset by the hierarchical env
+    b.lts = 0; b.dj = 0; b.dvj = 0; b.bps = 0; b.es = 0; b.jls = 0; b.alive = 0; b.dlts = 0;
+    b.hts = -5.0; b.drift = 0; b.cum_drift = 0; b.dhts = 0; b.cum_alive = 0;
+    b.level_rem = 5; b.n_high = 0; b.expect_high = 1;                       // :308-309
+    inc_frame(b, c, 2);                                                     // :312
+    float obs[42], js[NDOF];
+    int jal;
+    PostPhys<T> pp;
+    calc_state(st, b.wt, obs, js, jal, pp);                                 // :317
+    b.bxy[0] = pp.bx; b.bxy[1] = pp.by;
+    hier_high_obs(obs, b, pp.yaw, o44);                                     // :318
+}
+
+// updateRewardHigh (hier_env.py:524-536); returns the high-level reward (:627, :633)
+__device__ inline float hier_update_reward_high(Book& b) {
+    const double hts = -norm3_blas(b.target[0] - b.robot_pos[0], b.target[1] - b.robot_pos[1], b.target[2] - b.robot_pos[2]);
+    const double k = (double)(5 - b.level_rem + 1);
+    b.dhts = (hts - b.hts) / 0.0165;
+    b.dhts = b.dhts / k;
+    b.hts = hts;
+    b.drift = b.cum_drift / k;
+    b.cum_drift = 0;
+    return (float)(b.dhts * 0.3 + b.drift * 0.7);
+}
+
+// step(action_dict) (hier_env.py:355-366) -> high_level_step (:538-571) or low_level_step (:583-641), after the
+// physics of a low step; stores state/book and writes the dict-shaped outputs.
+template <typename T>
+__device__ void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsigned& ef) {
+    const ClipDev& c = a.clips[b.clip];
+    b.robot_pos[0] = b.bxy[0]; b.robot_pos[1] = b.bxy[1]; b.robot_pos[2] = 0;   // step(): :358-361
+    float obs[HUM_NOBS], js[NDOF], o44[HUM_NOBS_HIGH];
+    int jal;
+    PostPhys<T> pp;
+    unsigned agents = 0;
+    bool done = false;
+    float rew_low = 0.f, rew_high = 0.f;
+    if (high) {
+        // cur_obs is the last calc_state (same physics state, walk target before this call)
+        calc_state(st, b.wt, obs, js, jal, pp);
+        const float a0 = a.act_high[2 * (long)i], a1 = a.act_high[2 * (long)i + 1];
+        const float actionDegree = (float)atan2((double)a1, (double)a0) * (float)RAD2DEG;   // :540 (float32)
+        const double newDegree = (double)actionDegree + pp.yaw * RAD2DEG;                   // :543
+        b.hldt = newDegree * DEG2RAD;
+        const double ct = cos(b.hldt), sn = sin(b.hldt);
+        const double nw0 = b.robot_pos[0] + ct * 5, nw1 = b.robot_pos[1] + sn * 5, nw2 = b.robot_pos[2] + 0.0 * 5;
+        b.wt[0] = nw0; b.wt[1] = nw1;                                                       // :553
+        const double v0 = nw0 - b.robot_pos[0], v1 = nw1 - b.robot_pos[1], v2 = nw2 - b.robot_pos[2];
+        const double lenSEP = norm3_blas(b.sep[0] - b.robot_pos[0], b.sep[1] - b.robot_pos[1], b.sep[2] - b.robot_pos[2]);
+        const double nv = norm3_blas(v0, v1, v2);
+        b.sep[0] = (-v0 / nv) * lenSEP + b.robot_pos[0];                                    // :556-561
+        b.sep[1] = (-v1 / nv) * lenSEP + b.robot_pos[1];
+        b.sep[2] = (-v2 / nv) * lenSEP + b.robot_pos[2];
+        b.level_rem = 5;
+        b.n_high += 1;
+        b.expect_high = 0;
+        ref_obs(c, b.frame, obs + 42, ef);                                                  // :567 getLowLevelObs
+        agents = HUM_AGENT_LOW;
+    } else {
+        b.level_rem -= 1;                                                                   // :584
+        calc_state(st, b.wt, obs, js, jal, pp);                                             // :591
+        const float* act = a.act + (long)i * HUM_NACT;
+        // updateReward (:494-522)
+        double dJ = 0, dV = 0;
+#pragma unroll
+        for (int j = 0; j < NREF; j++) dJ = dJ + fabs(pp.q[JM_DOF[j]] - c.pos[b.frame * 14 + JM_COL[j]]) * JM_W[j];
+        int vrow = b.frame;
+        if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
+#pragma unroll
+        for (int j = 0; j < NREF; j++) dV = dV + fabs(pp.qd[JM_DOF[j]] - c.vel[vrow * 14 + JM_COL[j]]) * JM_WV[j];
+        const double jointScore = exp(4 * (-dJ / JOINT_WEIGHT_SUM));
+        const double jointVelScore = exp((-dV / JOINT_VEL_WEIGHT_SUM) / 2);
+        const double posture = exp(-((fabs(pp.yaw - b.hldt) + fabs(pp.roll)) + fabs(pp.pitch)));
+        b.dlts = (0.0 - b.lts) / 0.0165 * 0.1;                                              // lowTargetScore == 0
+        b.dj = jointScore;
+        b.dvj = jointVelScore;
+        b.lts = 0;
+        {
+            const float run = pairwise_sum_f<HUM_NACT>([&](int k) { return fabsf(act[k] * js[k]); }) / 17.0f;
+            const float stall = pairwise_sum_f<HUM_NACT>([&](int k) { return act[k] * act[k]; }) / 17.0f;
+            b.es = -1.0 * (double)run + -0.1 * (double)stall;
+        }
+        b.jls = -0.1 * jal;
+        b.alive = ((obs[0] + 0.8f) > 0.75f) ? 2.0 : -1.0;
+        b.cum_alive = b.cum_alive + b.alive;
+        b.bps = posture;
+        {                                                                                   // calcDriftScore :461-467
+            const double l0 = b.target[0] - b.srp[0], l1 = b.target[1] - b.srp[1], l2 = b.target[2] - b.srp[2];
+            const double lineLen = norm3_blas(l0, l1, l2);
+            double t = dot3_blas(b.robot_pos[0] - b.srp[0], b.robot_pos[1] - b.srp[1], b.robot_pos[2] - b.srp[2],
+                                 l0, l1, l2) / (lineLen * lineLen);
+            t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);   // np.clip keeps NaN
+            const double p0 = b.srp[0] + t * l0, p1 = b.srp[1] + t * l1, p2 = b.srp[2] + t * l2;
+            const double score = norm3_blas(p0 - b.robot_pos[0], p1 - b.robot_pos[1], p2 - b.robot_pos[2]);
+            b.cum_drift = b.cum_drift + exp(-6 * score);
+        }
+        double total = 0;                                                                   // :598-611
+        total = total + b.dj * REWARD_W[0];
+        total = total + b.dvj * REWARD_W[1];
+        total = total + b.dlts * REWARD_W[2];
+        total = total + b.es * REWARD_W[3];
+        total = total + b.jls * REWARD_W[4];
+        total = total + b.alive * REWARD_W[5];
+        total = total + b.bps * REWARD_W[6];
+        rew_low = (float)total;
+        inc_frame(b, c, 2);                                                                 // :613
+        {                                                                                   // checkTarget :469-487
+            const double dist = norm3_blas(b.robot_pos[0] - b.target[0], b.robot_pos[1] - b.target[1], b.robot_pos[2] - b.target[2]);
+            if (dist <= 0.5) {
+                const double rr = pp.yaw + (double)draw(a, i, b, -180, 180) * DEG2RAD;
+                double nt[3] = {b.robot_pos[0] + cos(rr) * 5, b.robot_pos[1] + sin(rr) * 5, b.robot_pos[2] + 0.0};
+                if ((b.mode & HUM_MODE_PREDEFINED) && a.npred > 0) {
+                    b.pred_idx = (b.pred_idx + 1) % a.npred;
+                    for (int k = 0; k < 3; k++) nt[k] = a.pred[3 * b.pred_idx + k];
+                }
+                for (int k = 0; k < 3; k++) { b.srp[k] = b.target[k]; b.target[k] = nt[k]; }
+                b.hts = -norm3_blas(b.target[0] - b.srp[0], b.target[1] - b.srp[1], b.target[2] - b.srp[2]);
+            }
+        }
+        const bool alive = b.alive > 0;                                                     // checkIfDone :573-581
+        const bool near = norm3_blas(b.target[0] - b.robot_pos[0], b.target[1] - b.robot_pos[1], b.target[2] - b.robot_pos[2]) <=
+                          norm3_blas(b.target[0] - b.srp[0], b.target[1] - b.srp[1], b.target[2] - b.srp[2]) + 1;
+        done = (b.mode & HUM_MODE_DEBUG) ? !alive : !(alive && near);
+        b.timestep += 1;
+        ref_obs(c, b.frame, obs + 42, ef);
+        if (done || b.timestep >= 3000) {                                                   // :624-630
+            done = true;
+            rew_high = hier_update_reward_high(b);
+            hier_high_obs(obs, b, pp.yaw, o44);
+            agents = HUM_AGENT_HIGH | HUM_AGENT_LOW;
+            b.cum_alive = 0;
+        } else if (b.level_rem <= 0) {                                                      // :631-636
+            rew_high = hier_update_reward_high(b);
+            hier_high_obs(obs, b, pp.yaw, o44);
+            agents = HUM_AGENT_HIGH;
+            b.cum_alive = 0;
+            b.expect_high = 1;
+        } else {
+            agents = HUM_AGENT_LOW;
+        }
+        b.bxy[0] = pp.bx; b.bxy[1] = pp.by;                                                 // flat_env.robot.body_xyz
+    }
+    if (agents & HUM_AGENT_LOW) {
+#pragma unroll
+        for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = obs[k];
+    }
+    if (agents & HUM_AGENT_HIGH) {
+#pragma unroll
+        for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high[(long)i * HUM_NOBS_HIGH + k] = o44[k];
+    }
+    a.rew[i] = (agents & HUM_AGENT_LOW) ? rew_low : 0.f;   // the level hand-back drops the low reward (:631-636)
+    a.rew_high[i] = rew_high;
+    a.agents[i] = (unsigned char)agents;
+    a.done[i] = done ? 1 : 0;
+    if (a.frame_out) a.frame_out[i] = b.frame;
+    if (done && (a.flags & HUM_STEP_AUTORESET)) {
+        float r44[HUM_NOBS_HIGH];
+        hier_reset_lane(a, i, st, b, -1, 0.0, r44, ef);
+        if (a.obs_high_reset) {
+#pragma unroll
+            for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high_reset[(long)i * HUM_NOBS_HIGH + k] = r44[k];
+        }
+    }
+    store_lane(a, i, st, b);
+    if (ef) atomicOr(a.eflags, ef);
+}
+
+// non-finite action on a lane (humanoid.py:55 assert): lane not stepped, flagged, outputs neutral
+__device__ inline void nonfinite_outputs(const KArgs& a, int i, int frame) {
+    if (!a.hier) {
+        for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = 0.f;
+    } else {
+        a.rew_high[i] = 0.f;
+        a.agents[i] = 0;
+    }
+    a.rew[i] = 0.f;
+    a.done[i] = 1;
+    if (a.frame_out) a.frame_out[i] = frame;
+}
+
+#pragma clang fp contract(on)
+
+
+// ----------------------------------------------------------------------------------- step
+template <typename T>
+__global__ void __launch_bounds__(256) step_kernel(KArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    T st[HUM_NSTATE];
+    Book b;
+    load_lane(a, i, st, b);
+    unsigned ef = 0;
+    // hierarchical env: the lane's acting agent (step(action_dict) dispatch, hier_env.py:363-366)
+    const bool high = a.hier && (a.agent_sel ? a.agent_sel[i] != 0 : b.expect_high != 0);
+    float act[HUM_NACT];
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < HUM_NACT; k++) {
+        act[k] = a.act[(long)i * HUM_NACT + k];
+        finite &= isfinite(act[k]);
+    }
+    if (!finite && !high) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
+        ef |= HUM_EFLAG_NONFINITE_ACTION;
+        nonfinite_outputs(a, i, b.frame);
+        atomicOr(a.eflags, ef);
+        return;
+    }
+    if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && !high) {
+        T tau[NDOF];
+#pragma unroll
+        for (int k = 0; k < HUM_NACT; k++) {   // apply_action: float(1 * power * 0.41 * clip(a)) in float32
+            const float g = (float)act_gain[k];
+            tau[act_dof[k]] = (T)(double)(g * fminf(fmaxf(act[k], -1.f), 1.f));
+        }
+        Lane<T> rows{(T*)a.scratch + i, (long)a.n};
+#pragma unroll 1
+        for (int s = 0; s < a.P.nsub; s++) {
+            if (substep(a.P, st, tau, rows)) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
+        }
+    }
+    if (a.hier) hier_post(a, i, st, b, high, ef);
+    else post_step(a, i, st, b, act, ef);
+}
+
+// Cooperative step: 16 lanes per env, EPB_ envs per block of EPB_*16 threads (one wavefront), env working
+// set in LDS.  EPB_ = 4 fills the wave; EPB_ = 2 leaves half of it idle but lets a SIMD hold two waves
+// (19.3 KB LDS per block), so one wave's LDS/memory waits overlap the other's VALU issue.
+template <typename T, int EPB_>
+__global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
+    __shared__ GroupLDS<T> sh[EPB_];
+    const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
+    const int i = blockIdx.x * EPB_ + ge;
+    const bool valid = i < a.n;
+    GroupLDS<T>& S = sh[ge];
+    const ModelTab<T>& M = tab<T>();
+    for (int e = l; e < HUM_NSTATE; e += GL)
+        S.st[e] = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
+    bool fin = true;
+    for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60), float32 product
+        const float av = valid ? a.act[(long)i * HUM_NACT + k] : 0.f;
+        fin = fin && isfinite(av);
+        S.tau[M.act_dof[k]] = (T)(double)(M.act_gain[k] * fminf(fmaxf(isfinite(av) ? av : 0.f, -1.f), 1.f));
+    }
+    const int gbit = (threadIdx.x & 63) & ~(GL - 1);
+    // hierarchical env: envs whose acting agent is the high level take no physics step (hier_env.py:538-571)
+    const bool high = a.hier && valid && (a.agent_sel ? a.agent_sel[i] != 0 : a.bi[10 * a.n + i] != 0);
+    const bool env_ok = high || ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
+    const bool any_phys = __ballot(valid && !high) != 0;   // wave-uniform
+    __syncthreads();
+    unsigned ef = 0;
+    if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
+#pragma unroll 1
+        for (int s = 0; s < a.P.nsub; s++)
+            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * EPB_ * GROW_PER_ENV, l, ef);
+    }
+    PHASE_INIT;
+    if (valid && l == 0) {
+        Book b;
+        load_book(a, i, b);
+        if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
+            ef |= HUM_EFLAG_NONFINITE_ACTION;
+            nonfinite_outputs(a, i, b.frame);
+        } else {
+            T st[HUM_NSTATE];
+            if (high) {   // physics (if the wave ran it) is discarded: the HBM state is the current one
+#pragma unroll
+                for (int e = 0; e < HUM_NSTATE; e++) st[e] = ((const T*)a.phys)[(long)e * a.n + i];
+            } else {
+#pragma unroll
+                for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
+            }
+            if (a.hier) {
+                hier_post(a, i, st, b, high, ef);
+            } else {
+                float act[HUM_NACT];
+#pragma unroll
+                for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[(long)i * HUM_NACT + k];
+                post_step(a, i, st, b, act, ef);
+            }
+        }
+    }
+    PHASE(10);
+    if (ef) atomicOr(a.eflags, ef);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) reset_kernel(KArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    if (a.mask && !a.mask[i]) return;
+    T st[HUM_NSTATE];
+    Book b;
+    load_lane(a, i, st, b);
+    unsigned ef = 0;
+    float obs[HUM_NOBS];
+    const int sf = a.start_frame ? a.start_frame[i] : -1;
+    const double ry = a.reset_yaw ? a.reset_yaw[i] : 0.0;
+    if (a.hier) {
+        hier_reset_lane(a, i, st, b, sf, ry, obs, ef);
+        if (a.obs_high) {
+#pragma unroll
+            for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high[(long)i * HUM_NOBS_HIGH + k] = obs[k];
+        }
+    } else {
+        reset_lane(a, i, st, b, sf, ry, obs, ef);
+        if (a.obs) {
+#pragma unroll
+            for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = obs[k];
+        }
+    }
+    store_lane(a, i, st, b);
+    if (ef) atomicOr(a.eflags, ef);
+}
+
+static __global__ void init_kernel(KArgs a) {   // fresh lanes: clip 0, no mode, RNG key from (seed, global lane)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const unsigned long long k = splitmix64(a.seed + (unsigned long long)(a.lane_offset + i));
+    a.bi[6 * a.n + i] = (int)(unsigned)(k & 0xffffffffull);
+    a.bi[7 * a.n + i] = (int)(unsigned)(k >> 32);
+}
+
+template <typename T>
+__global__ void aux_kernel(KArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    T st[HUM_NSTATE];
+    Book b;
+    load_lane(a, i, st, b);
+    float* o = a.aux + (long)i * HUM_NAUX;
+    o[HUM_AUX_DELTA_JOINTS] = (float)b.dj;
+    o[HUM_AUX_DELTA_END_POINTS] = 0.f;   // calcEndPointScore is not on the reward path (:445)
+    o[HUM_AUX_LOW_TARGET_SCORE] = (float)b.lts;
+    o[HUM_AUX_DELTA_VEL_JOINTS] = (float)b.dvj;
+    o[HUM_AUX_BODY_POSTURE] = (float)b.bps;
+    o[HUM_AUX_HIGH_TARGET_SCORE] = a.hier ? (float)b.hts : 0.f;
+    o[HUM_AUX_DRIFT_SCORE] = a.hier ? (float)b.drift : 0.f;
+    o[HUM_AUX_BASE_REWARD] = 0.f;
+    o[HUM_AUX_ALIVE] = (float)b.alive;
+    o[HUM_AUX_ELECTRICITY] = (float)b.es;
+    o[HUM_AUX_JOINT_LIMIT] = (float)b.jls;
+    o[HUM_AUX_DIST_FROM_ORIGIN] = (float)norm3_blas(b.robot_pos[0], b.robot_pos[1], b.robot_pos[2]);
+}
+
+template <typename T>
+__global__ void parts_kernel(KArgs a, double* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    T st[HUM_NSTATE];
+    Book b;
+    load_lane(a, i, st, b);
+    Kin<T> K;
+    forward_kinematics(st + 3, st + 13, K);
+    T pp[NPART][3];
+    part_positions(K, pp);
+    for (int k = 0; k < NPART; k++)
+        for (int e = 0; e < 3; e++)
+            out[((long)i * NPART + k) * 3 + e] = part_body[k] < 0 ? 0.0 : (double)st[e] + (double)pp[k][e];
+}
+
+
+// the benchmarked cooperative kernel lives in its own translation unit (group_f32.hip)
+hipError_t launch_group_f32_4(const KArgs& a, int nblocks, hipStream_t s);
+
+}  // namespace hkk

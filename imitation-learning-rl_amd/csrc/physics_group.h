@@ -9,7 +9,7 @@
 //   FK              every lane (registers), lane 0 publishes R/o/u to LDS
 //   ABA pass 1      lane b = body b: velocity, bias acceleration, spatial inertia, bias force
 //   ABA pass 2      by tree level (4 steps, one body per 4-lane group), children summed by the parent
-//   ABA pass 3      every lane redundantly (tiny), lane 0 publishes accelerations
+//   ABA pass 3      base on every lane, then by tree level (root -> leaves), groups integrate their dofs
 //   limits/contacts lane-parallel candidate tests, ballot-compacted in the oracle's order
 //   rows            one constraint row per lane: Jacobian + test-impulse response M^-1 J^T
 //   PGS             rows in Bullet order; J.nu over the 16 lanes by DPP row_ror reductions
@@ -21,8 +21,9 @@ namespace hk {
 constexpr int GL = 16;                       // lanes per env
 constexpr int MAXC_G = 16;                   // contact cap of the cooperative kernel
 constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // 65 rows
-constexpr int RW = 2 * NV + 7;               // J[NV], M[NV], b, lo, hi, lam, meff, mu, 0 (pad read by lanes
-                                             // without a second nu component: branch-free PGS loads)
+constexpr int RW = 2 * NV + 8;               // J[NV], M[NV], b, lo, hi, lam, meff, mu, 0 (pad read by lanes
+                                             // without a second nu component: branch-free PGS loads),
+                                             // byte offset of the friction row's normal lambda (int bits)
 constexpr int NCAND_GROUND = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 1 : 2; return n; }();
 constexpr int NCAND = NCAND_GROUND + NPAIR;
 
@@ -88,8 +89,8 @@ constexpr ModelTab<T> make_tab() {
     return m;
 }
 
-__constant__ ModelTab<float> kTabF = make_tab<float>();
-__constant__ ModelTab<double> kTabD = make_tab<double>();
+static __constant__ ModelTab<float> kTabF = make_tab<float>();   // per translation unit
+static __constant__ ModelTab<double> kTabD = make_tab<double>();
 template <typename T> __device__ inline const ModelTab<T>& tab();
 template <> __device__ inline const ModelTab<float>& tab<float>() { return kTabF; }
 template <> __device__ inline const ModelTab<double>& tab<double>() { return kTabD; }
@@ -106,7 +107,7 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
     T U[NDOF][6], Dinv[NB][9], L0[21];
     union {
         struct {   // articulated-body pass (dead once the accelerations are known)
-            T V[NB][6], c[NB][6], IA[NB][21], pA[NB][6], uu[NDOF + 1];
+            T V[NB][6], c[NB][6], IA[NB][21], pA[NB][6], uu[NDOF + 1];   // V: pass-3 body accelerations
         } aba;
         struct {   // contacts + constraint rows
             T gp[NGEOM][2][3];
@@ -129,6 +130,9 @@ __device__ unsigned long long g_phase_cycles[16];
         }                                                                        \
     } while (0)
 #define PHASE_INIT unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
+#elif defined(HUM_PHASE_MARK)   // static ISA attribution (tools/isa_phases.py): asm comments at phase ends
+#define PHASE(k) asm volatile("; @phase " #k ::: "memory")
+#define PHASE_INIT do { } while (0)
 #else
 #define PHASE(k) do { } while (0)
 #define PHASE_INIT do { } while (0)
@@ -140,12 +144,16 @@ __device__ inline void wave_sync() {   // cross-lane LDS ordering inside one wav
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ inline float med3(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+__device__ inline double med3(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
+
 // 16-lane (DPP row) all-reduce sum
 __device__ inline float row_sum(float v) {
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror:8
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror:4
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xF, 0xF, false));  // row_ror:2
-    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false));  // row_ror:1
+    // update_dpp with old = 0 / bound_ctrl lets the compiler fold each step into one v_add_f32_dpp
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true));  // row_ror:8
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, true));  // row_ror:4
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, true));  // row_ror:2
+    v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, true));  // row_ror:1
     return v;
 }
 template <int CTRL>
@@ -161,6 +169,44 @@ __device__ inline double row_sum(double v) {
     v += mov_dpp_d<0x122>(v);
     v += mov_dpp_d<0x121>(v);
     return v;
+}
+
+// 6x6 Cholesky with the inverse of each pivot stored on the diagonal: the solves (base step, and one per
+// constraint row in g_response) multiply instead of dividing (an IEEE fp32 divide is ~10 VALU)
+template <typename T>
+__device__ inline void chol6_inv(const T* A, T* L) {
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        T s = A[sidx(j, j)];
+#pragma unroll
+        for (int k = 0; k < j; k++) s -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+        const T inv = T(1) / sqrt(s);
+        L[j * (j + 1) / 2 + j] = inv;
+#pragma unroll
+        for (int i = j + 1; i < 6; i++) {
+            T t = A[sidx(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; k++) t -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+            L[i * (i + 1) / 2 + j] = t * inv;
+        }
+    }
+}
+template <typename T>
+__device__ inline void chol6_solve_inv(const T* L, T* b) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        T s = b[i];
+#pragma unroll
+        for (int k = 0; k < i; k++) s -= L[i * (i + 1) / 2 + k] * b[k];
+        b[i] = s * L[i * (i + 1) / 2 + i];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
+        T s = b[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) s -= L[k * (k + 1) / 2 + i] * b[k];
+        b[i] = s * L[i * (i + 1) / 2 + i];
+    }
 }
 
 // ------------------------------------------------------------------------- test-impulse response
@@ -210,7 +256,7 @@ __device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int
         T L[21];
 #pragma unroll
         for (int q = 0; q < 21; q++) L[q] = S.L0[q];
-        chol6_solve(L, a[0]);
+        chol6_solve_inv(L, a[0]);
     }
 #pragma unroll
     for (int e = 0; e < 6; e++) out[e] = a[0][e];
@@ -264,6 +310,52 @@ __device__ inline void g_row_jacobian(const GroupLDS<T>& S, int b, const T* f, T
     }
 }
 
+// J row for spatial forces fa on body ba and fb on body bb (either < 0 = absent), one pass over the dofs
+template <typename T>
+__device__ inline void g_row_jacobian2(const GroupLDS<T>& S, int ba, const T* fa, int bb, const T* fb, T* J) {
+    const ModelTab<T>& M = tab<T>();
+#pragma unroll
+    for (int e = 0; e < 6; e++) J[e] = (ba >= 0 ? fa[e] : T(0)) + (bb >= 0 ? fb[e] : T(0));
+#pragma unroll
+    for (int x = 1; x < NB; x++) {
+        const bool ona = ba >= 0 && M.onpath[ba < 0 ? 0 : ba][x];
+        const bool onb = bb >= 0 && M.onpath[bb < 0 ? 0 : bb][x];
+#pragma unroll
+        for (int k = 0; k < body_ndof[x]; k++) {
+            const int d = body_dof0[x] + k;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[x], S.u[d], Sc + 3);
+            T sa = 0, sb = 0;
+#pragma unroll
+            for (int e = 0; e < 6; e++) { sa += fa[e] * Sc[e]; sb += fb[e] * Sc[e]; }
+            J[6 + d] = (ona ? sa : T(0)) + (onb ? sb : T(0));
+        }
+    }
+}
+
+// spatial velocities of bodies ba and bb (bb < 0: Vb = 0) from nu, one pass over the dofs
+template <typename T>
+__device__ inline void g_body_vel2(const GroupLDS<T>& S, int ba, int bb, T* Va, T* Vb) {
+    const ModelTab<T>& M = tab<T>();
+#pragma unroll
+    for (int e = 0; e < 6; e++) { Va[e] = S.nu[e]; Vb[e] = bb >= 0 ? S.nu[e] : T(0); }
+#pragma unroll
+    for (int x = 1; x < NB; x++) {
+        const bool ona = ba >= 0 && M.onpath[ba < 0 ? 0 : ba][x];
+        const bool onb = bb >= 0 && M.onpath[bb < 0 ? 0 : bb][x];
+#pragma unroll
+        for (int k = 0; k < body_ndof[x]; k++) {
+            const int d = body_dof0[x] + k;
+            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+            cross3(S.o[x], S.u[d], Sc + 3);
+            const T qd = S.nu[6 + d];
+            const T qa = ona ? qd : T(0), qb = onb ? qd : T(0);
+#pragma unroll
+            for (int e = 0; e < 6; e++) { Va[e] += Sc[e] * qa; Vb[e] += Sc[e] * qb; }
+        }
+    }
+}
+
 // spatial velocity of body b from the generalised velocity nu (LDS)
 template <typename T>
 __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
@@ -290,11 +382,12 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
 // Row t of the wave's concatenated row list (env 0's rows, then env 1's, ...) goes to lane t % (16 EPB_):
 // per-env counts are wave-uniform (readlane), so the env/row of a task is two compares away.
 template <typename T>
-__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc) {
+__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc, int nrm_off) {
 #pragma unroll
     for (int q = 0; q < NV; q++) { R[q] = J[q]; R[NV + q] = Mi[q]; }
 #pragma unroll
     for (int q = 0; q < 7; q++) R[2 * NV + q] = sc[q];
+    *reinterpret_cast<int*>(R + 2 * NV + 7) = nrm_off;   // slot 2NV+7 of a T row
 }
 template <typename T>
 __device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J, const T* Mi, const T* sc) {
@@ -331,51 +424,40 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             if (q == e) { r = t - pre[q]; enl = nls[q]; enc = ncs[q]; }
         const GroupLDS<T>& S = shb[e];
         const auto& C = S.x.cr;
+        // every row type (limit / normal / friction) funnels into ONE test-impulse response call: the wave's
+        // lanes hold mixed row types, so separate calls per branch would all execute
         T J[NV], Mi[NV], sc[7];
-#pragma unroll
-        for (int q = 0; q < NV; q++) J[q] = 0;
-        if (r < enl) {
+        int ba = -1, bb = -1, jd = -1;
+        T fa[6] = {0, 0, 0, 0, 0, 0}, fb[6] = {0, 0, 0, 0, 0, 0}, jsign = 0;
+        const bool lim = r < enl;
+        if (lim) {
             const int d = C.rdesc[r] & 0xff, side = C.rdesc[r] >> 8;
             const T sg = side == 0 ? T(1) : T(-1);
             const T q = S.st[13 + d];
             const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
-            g_response(S, -1, (const T*)nullptr, -1, (const T*)nullptr, d, sg, Mi);
-#pragma unroll
-            for (int k = 0; k < NV; k++) J[k] = (k == 6 + d) ? sg : T(0);
-            T mdd = 0;
-#pragma unroll
-            for (int k = 0; k < NDOF; k++) if (k == d) mdd = Mi[6 + k];
+            jd = d;
+            jsign = sg;
             sc[0] = -pen * (T)P.erp_limit / dt;
-            sc[1] = 0;
             sc[2] = (T)P.limit_max_impulse;
-            sc[3] = 0;
-            sc[4] = T(1) / (sg * mdd);
             sc[5] = 0;
-            sc[6] = 0;
         } else {
             const int cidx = r < enl + enc ? r - enl : (r - enl - enc) >> 1;
             const int f = r < enl + enc ? 0 : 1 + ((r - enl - enc) & 1);
             const T* ce = C.con[cidx];
-            const int ba = (int)ce[0], bb = (int)ce[1];
+            ba = (int)ce[0];
+            bb = (int)ce[1];
             const T pa[3] = {ce[2], ce[3], ce[4]}, pb[3] = {ce[5], ce[6], ce[7]}, n[3] = {ce[8], ce[9], ce[10]};
             const T d = ce[11];
             T dir[3];
             if (f == 0) {
                 dir[0] = n[0]; dir[1] = n[1]; dir[2] = n[2];
             } else {
-                T Va[6], Vb[6], va[3], vb[3] = {0, 0, 0}, vr[3];
-                g_body_vel(S, ba, Va);
+                T Va[6], Vb[6], va[3], vb[3], vr[3];
+                g_body_vel2(S, ba, bb, Va, Vb);
                 cross3(Va, pa, va);
+                cross3(Vb, pb, vb);
 #pragma unroll
-                for (int i = 0; i < 3; i++) va[i] += Va[3 + i];
-                if (bb >= 0) {
-                    g_body_vel(S, bb, Vb);
-                    cross3(Vb, pb, vb);
-#pragma unroll
-                    for (int i = 0; i < 3; i++) vb[i] += Vb[3 + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 3; i++) vr[i] = va[i] - vb[i];
+                for (int i = 0; i < 3; i++) vr[i] = (va[i] + Va[3 + i]) - (vb[i] + Vb[3 + i]);
                 const T vn = dot3(vr, n);
                 T lat[3], t1[3], t2[3];
 #pragma unroll
@@ -392,25 +474,32 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
 #pragma unroll
                 for (int i = 0; i < 3; i++) dir[i] = f == 1 ? t1[i] : t2[i];
             }
-            T fa[6], fb[6];
             cross3(pa, dir, fa); fa[3] = dir[0]; fa[4] = dir[1]; fa[5] = dir[2];
-            cross3(pb, dir, fb);
-            fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
-            g_row_jacobian(S, ba, fa, T(1), J);
-            if (bb >= 0) g_row_jacobian(S, bb, fb, T(1), J);
-            g_response(S, ba, fa, bb, fb, -1, T(0), Mi);
-            T jm = 0;
-#pragma unroll
-            for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];
+            if (bb >= 0) {
+                cross3(pb, dir, fb);
+                fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
+            }
             sc[0] = f == 0 ? (d > 0 ? -d / dt : -d * (T)P.erp_contact / dt) : T(0);
-            sc[1] = 0;
-            sc[2] = (T)1e10;
-            sc[3] = 0;
-            sc[4] = T(1) / jm;
-            sc[5] = bb >= 0 ? (T)P.mu_self : (T)P.mu_ground;
-            sc[6] = 0;
+            sc[2] = f == 0 ? (T)1e10 : T(0);   // friction rows: bounds come from mu * lambda_n in the PGS
+            sc[5] = f == 0 ? T(0) : (bb >= 0 ? (T)P.mu_self : (T)P.mu_ground);   // friction rows only
         }
-        if (r < MAXR_LDS) store_row(shb[e].x.cr.row[r], J, Mi, sc);
+        g_row_jacobian2(S, ba, fa, bb, fb, J);   // limit rows: ba = bb = -1 -> J = 0 (unit entry below)
+#pragma unroll
+        for (int k = 0; k < NDOF; k++)
+            if (k == jd) J[6 + k] = jsign;
+        g_response(S, ba, fa, bb, fb, jd, jsign, Mi);
+        T jm = 0;
+#pragma unroll
+        for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];   // limit rows: sg * Mi[6 + d] (sg^2 = 1)
+        sc[1] = 0;
+        sc[3] = 0;
+        sc[4] = T(1) / jm;
+        sc[6] = 0;
+        // PGS: byte offset (from row 0) of the lambda bounding this row - its normal row for a friction row,
+        // any row (row 0) otherwise (mu = 0 there)
+        const int nrm = r >= enl + enc ? (r + enl - enc) >> 1 : 0;
+        const int nrm_off = (nrm < MAXR_LDS ? nrm : 0) * RW * (int)sizeof(T) + (2 * NV + 3) * (int)sizeof(T);
+        if (r < MAXR_LDS) store_row(shb[e].x.cr.row[r], J, Mi, sc, nrm_off);
         else store_row_global(grow_block + (long)e * GROW_PER_ENV + (r - MAXR_LDS) * RW, J, Mi, sc);
     }
 }
@@ -525,6 +614,53 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
     }
 #pragma unroll
     for (int q = 0; q < 9; q++) S.Dinv[b][q] = Di[q];
+}
+
+// ------------------------------------------------------------------------- ABA pass 3, one tree level
+// Root -> leaves: {lwaist, upper arms} -> {pelvis, lower arms} -> {thighs} -> {shins}; body accelerations
+// travel through the dead pass-1 velocity slots A.V.  Each group integrates its own dofs into nu*
+// (groups sharing a body compute and write identical values).
+constexpr int FWD_BODY[4][4] = {{1, 7, 9, 9}, {2, 8, 10, 10}, {3, 5, 3, 5}, {4, 6, 4, 6}};
+template <typename T, int LV>
+__device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt) {
+    auto& A = S.x.aba;
+    auto sel = [&](auto f) {
+        const int v0 = f(FWD_BODY[LV][0]), v1 = f(FWD_BODY[LV][1]), v2 = f(FWD_BODY[LV][2]), v3 = f(FWD_BODY[LV][3]);
+        return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+    };
+    const int b = sel([](int x) { return x; });
+    const int p = sel([](int x) { return body_parent[x]; });
+    const int k = sel([](int x) { return body_ndof[x]; });
+    const int d0 = sel([](int x) { return body_dof0[x]; });
+    const T vmax = (T)P.max_coord_vel;
+    T ap[6], r[3], ab[6];
+#pragma unroll
+    for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + A.c[b][e]; ab[e] = ap[e]; }
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int d = j < k ? d0 + j : d0;
+        T t = A.uu[d];
+#pragma unroll
+        for (int e = 0; e < 6; e++) t -= S.U[d][e] * ap[e];
+        r[j] = j < k ? t : T(0);
+    }
+    const T ob[3] = {S.o[b][0], S.o[b][1], S.o[b][2]};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        T t = 0;
+#pragma unroll
+        for (int j = 0; j < 3; j++) t += S.Dinv[b][3 * i + j] * r[j];   // padded block: identity, r = 0
+        const int d = i < k ? d0 + i : d0;
+        T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
+        cross3(ob, Sc, Sc + 3);
+        const T qdd = i < k ? t : T(0);
+#pragma unroll
+        for (int e = 0; e < 6; e++) ab[e] += Sc[e] * qdd;
+        const T nn = clampT(S.nu[6 + d] + dt * qdd, -vmax, vmax);
+        if (i < k) S.nu[6 + d] = nn;
+    }
+#pragma unroll
+    for (int e = 0; e < 6; e++) A.V[b][e] = ab[e];
 }
 
 // ------------------------------------------------------------------------- one cooperative substep
@@ -657,7 +793,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (int i = 0; i < 3; i++) { pA[i] -= n[i] + cxF[i]; pA[3 + i] -= F[i]; }
         }
 #pragma unroll
-        for (int e = 0; e < 6; e++) { S.x.aba.V[b][e] = V[e]; S.x.aba.c[b][e] = cb[e]; S.x.aba.pA[b][e] = pA[e]; }
+        for (int e = 0; e < 6; e++) { S.x.aba.c[b][e] = cb[e]; S.x.aba.pA[b][e] = pA[e]; }
 #pragma unroll
         for (int q = 0; q < 21; q++) S.x.aba.IA[b][q] = IA[q];
     }
@@ -681,57 +817,40 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     PHASE(3);
     // ---- base + pass 3 (redundant on every lane); lane 0 publishes L0 and nu* = clamp(nu + dt acc)
     {
-        T L[21], a[NB][6];
-        T IA0[21];
+        // base (redundant on every lane), then the forward pass by tree level (root -> leaves, one body per
+        // 4-lane group, see group_fwd_level); lane 0 integrates the base and publishes L0 (inverse-diagonal form)
+        const T vmax = (T)P.max_coord_vel;
+        T L[21], a0[6], IA0[21], nub[6];
 #pragma unroll
         for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q] + A.IA[1][q] + A.IA[7][q] + A.IA[9][q];   // torso + kids
-        chol6(IA0, L);
+        chol6_inv(IA0, L);
 #pragma unroll
-        for (int e = 0; e < 6; e++) a[0][e] = -(A.pA[0][e] + A.pA[1][e] + A.pA[7][e] + A.pA[9][e]);
-        chol6_solve(L, a[0]);
-        T acc[NV];
+        for (int e = 0; e < 6; e++) a0[e] = -(A.pA[0][e] + A.pA[1][e] + A.pA[7][e] + A.pA[9][e]);
+        chol6_solve_inv(L, a0);
 #pragma unroll
-        for (int b = 1; b < NB; b++) {
-            const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
-            T ap[6], r[3];
-#pragma unroll
-            for (int e = 0; e < 6; e++) ap[e] = a[p][e] + A.c[b][e];
-#pragma unroll
-            for (int j = 0; j < k; j++) {
-                T t = A.uu[d0 + j];
-#pragma unroll
-                for (int e = 0; e < 6; e++) t -= S.U[d0 + j][e] * ap[e];
-                r[j] = t;
-            }
-#pragma unroll
-            for (int e = 0; e < 6; e++) a[b][e] = ap[e];
-#pragma unroll
-            for (int i = 0; i < k; i++) {
-                T t = 0;
-#pragma unroll
-                for (int j = 0; j < k; j++) t += S.Dinv[b][3 * i + j] * r[j];
-                acc[6 + d0 + i] = t;
-                const int d = d0 + i;
-                T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-                cross3(S.o[b], S.u[d], Sc + 3);
-#pragma unroll
-                for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * t;
-            }
-        }
-        T nu[NV];
-#pragma unroll
-        for (int e = 0; e < NV; e++) nu[e] = S.nu[e];
-        T wxv[3];
-        cross3(nu, nu + 3, wxv);
-#pragma unroll
-        for (int i = 0; i < 3; i++) { acc[i] = a[0][i]; acc[3 + i] = a[0][3 + i] + wxv[i]; }
-        __syncthreads();   // every lane has read the ABA union and nu
+        for (int e = 0; e < 6; e++) nub[e] = S.nu[e];
         if (l == 0) {
-            const T vmax = (T)P.max_coord_vel;
+#pragma unroll
+            for (int e = 0; e < 6; e++) A.V[0][e] = a0[e];
+        }
+        wave_sync();
+        group_fwd_level<T, 0>(P, S, l >> 2, dt);
+        wave_sync();
+        group_fwd_level<T, 1>(P, S, l >> 2, dt);
+        wave_sync();
+        group_fwd_level<T, 2>(P, S, l >> 2, dt);
+        wave_sync();
+        group_fwd_level<T, 3>(P, S, l >> 2, dt);
+        if (l == 0) {
+            T wxv[3];
+            cross3(nub, nub + 3, wxv);
 #pragma unroll
             for (int q = 0; q < 21; q++) S.L0[q] = L[q];
 #pragma unroll
-            for (int e = 0; e < NV; e++) S.nu[e] = clampT(nu[e] + dt * acc[e], -vmax, vmax);
+            for (int i = 0; i < 3; i++) {
+                S.nu[i] = clampT(nub[i] + dt * a0[i], -vmax, vmax);
+                S.nu[3 + i] = clampT(nub[3 + i] + dt * (a0[3 + i] + wxv[i]), -vmax, vmax);
+            }
         }
     }
     __syncthreads();
@@ -872,67 +991,62 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
     //      re-reads values it wrote itself, so no cross-lane LDS ordering is needed inside the loop.
     T n0 = S.nu[l], n1 = l < NV - GL ? S.nu[GL + l] : T(0);
-    if (__ballot(nrows > MAXR_LDS) == 0) {
-        // Common case (every env of the wave keeps its rows in LDS): software-pipelined over the flattened
-        // (iteration, row) sequence - the next row's J / M^-1 J^T entries, scalars, lambda and (friction)
-        // normal lambda are read while the current row's 16-lane DPP reduction runs; the only values the
-        // current row can change for the next one (its own lambda when nrows == 1, or the normal lambda of
-        // the next friction row) are patched in registers.
-        struct RowRegs { T j0, j1, m0, m1, b, lo, hi, lam, meff, mu, ln; int nrm; };
+#ifndef HUM_PGS_SLOW
+    if (__ballot(nrows > MAXR_LDS || nrows == 1) == 0) {
+#else
+    if (false) {
+#endif
+        // Common case (every env of the wave keeps >= 2 rows, all in LDS): software-pipelined over the
+        // flattened (iteration, row) sequence with ping-pong register sets - the next row's J / M^-1 J^T
+        // entries and scalars are read while the current row's 16-lane DPP reduction runs; the friction
+        // rows' normal lambda is read right after the previous row's lambda store (LDS ops of a wave are
+        // ordered), so it sees the update when that row was its normal.  Branch-free bounds: normal and
+        // limit rows store mu = 0, friction rows lo = hi = 0, so [lo - mu ln, hi + mu ln] is exact for all.
+        struct RowRegs { T j0, j1, m0, m1, b, lo, hi, lam, meff, mu; int nrm_off; };
+        const T* rowbase = &C.row[0][0];
         // lanes without a second nu component read the row's zero pad: no branch or select on loaded values
         const int lj1 = l < NV - GL ? GL + l : 2 * NV + 6, lm1 = l < NV - GL ? NV + GL + l : 2 * NV + 6;
-        auto load = [&](int r, RowRegs& d) {
-            const T* R = C.row[r];
+        auto load = [&](const T* R, RowRegs& d) {
             d.j0 = R[l];
             d.j1 = R[lj1];
             d.m0 = R[NV + l];
             d.m1 = R[lm1];
             d.b = R[2 * NV + 0]; d.lo = R[2 * NV + 1]; d.hi = R[2 * NV + 2]; d.lam = R[2 * NV + 3];
             d.meff = R[2 * NV + 4]; d.mu = R[2 * NV + 5];
-            d.nrm = r >= nl + nc ? nl + ((r - nl - nc) >> 1) : -1;   // friction row -> its normal row
-            d.ln = C.row[d.nrm >= 0 ? d.nrm : 0][2 * NV + 3];
+            d.nrm_off = *reinterpret_cast<const int*>(R + 2 * NV + 7);
         };
-        // one Gauss-Seidel row update; `patch_*` substitute the lambda the previous row just produced for a
-        // value that was prefetched before it was written (its own lambda when nrows == 1, or the normal
-        // lambda of a friction row whose normal row was the previous one)
-        auto update = [&](RowRegs& d, int r, bool patch_lam, bool patch_ln, T prev) -> T {
-            if (patch_lam) d.lam = prev;
-            if (patch_ln) d.ln = prev;
-            T lo = d.lo, hi = d.hi;
-            if (d.nrm >= 0) {   // friction bounds from the normal impulse of the same contact
-                lo = -d.mu * d.ln;
-                hi = d.mu * d.ln;
-            }
-            const T part = d.j0 * n0 + d.j1 * n1;
-            const T jv = row_sum(part);
-            const T lnew = clampT(d.lam + d.meff * (d.b - jv), lo, hi);
-            C.row[r][2 * NV + 3] = lnew;
+        auto load_ln = [&](const RowRegs& d) -> T {   // normal lambda (byte offset precomputed per row)
+            return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(rowbase) + d.nrm_off);
+        };
+        auto update = [&](const RowRegs& d, T ln, T* R) {
+            const T lo = d.lo - d.mu * ln, hi = d.hi + d.mu * ln;
+            const T jv = row_sum(d.j0 * n0 + d.j1 * n1);
+            const T lnew = med3(d.lam + d.meff * (d.b - jv), lo, hi);   // == clamp: lo <= hi always
+            R[2 * NV + 3] = lnew;
             const T dl = lnew - d.lam;
             n0 += d.m0 * dl;
             n1 += d.m1 * dl;
-            return lnew;
         };
         const int total = P.iters * nrows;
         if (total > 0) {
-            // ping-pong register sets A/B, loads issued unconditionally one row ahead (no phi copies that
-            // would force the loads to complete early)
             RowRegs A, B;
-            load(0, A);
+            const T* RA = rowbase;
+            load(RA, A);
+            T lnA = load_ln(A), lnB;
             int r = 0;
-            bool pa_lam = false, pa_ln = false;
-            T prev = 0;
             for (int k = 0;; k += 2) {
                 int rn = r + 1 == nrows ? 0 : r + 1;
-                load(rn, B);
-                bool pb_lam = rn == r, pb_ln = B.nrm == r;
-                prev = update(A, r, pa_lam, pa_ln, prev);
+                const T* RB = rowbase + rn * RW;
+                load(RB, B);
+                update(A, lnA, const_cast<T*>(RA));
+                lnB = load_ln(B);
                 if (k + 1 >= total) break;
                 r = rn;
                 rn = r + 1 == nrows ? 0 : r + 1;
-                load(rn, A);
-                pa_lam = rn == r;
-                pa_ln = A.nrm == r;
-                prev = update(B, r, pb_lam, pb_ln, prev);
+                RA = rowbase + rn * RW;
+                load(RA, A);
+                update(B, lnB, const_cast<T*>(RB));
+                lnA = load_ln(A);
                 if (k + 2 >= total) break;
                 r = rn;
             }
