@@ -53,6 +53,13 @@ struct hum_env {
 };
 
 namespace {
+// block row pool capacity of the cooperative kernel: envs_per_block * MAXR_LDS LDS row slots, or fewer when
+// hum_config.lds_rows asks (tests of the global spill path)
+static int lds_rows_of(const hum_config& c) {
+    const int pool = c.envs_per_block * MAXR_LDS;
+    return c.lds_rows > 0 && c.lds_rows < pool ? c.lds_rows : pool;
+}
+
 KArgs make_args(hum_env* e) {
     KArgs a;
     memset(&a, 0, sizeof a);
@@ -76,6 +83,7 @@ KArgs make_args(hum_env* e) {
     a.P.max_contacts = c.max_contacts;
     a.P.self_collision = c.self_collision;
     a.P.joint_damping = c.joint_damping;
+    a.P.lds_rows = lds_rows_of(c);
     a.hier = c.hier;
     a.clips = e->clips_dev;
     a.pred = e->pred;
@@ -130,6 +138,7 @@ void hum_default_config(hum_config* c) {
     c->kernel = 1;
     c->hier = 0;
     c->envs_per_block = 4;
+    c->lds_rows = 0;
 }
 
 int hum_create(const hum_config* cfg, hum_env** out) {
@@ -143,6 +152,7 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (cfg->hier != 0 && cfg->hier != 1) return fail(HUM_ERR_ARG, "hum_create: hier must be 0 or 1");
     if (cfg->envs_per_block != 1 && cfg->envs_per_block != 2 && cfg->envs_per_block != 4)
         return fail(HUM_ERR_ARG, "hum_create: envs_per_block must be 1, 2 or 4");
+    if (cfg->lds_rows < 0) return fail(HUM_ERR_ARG, "hum_create: lds_rows must be >= 0");
     if (cfg->max_contacts < 0 || cfg->max_contacts > (cfg->kernel == 1 ? MAXC_G : MAXC))
         return fail(HUM_ERR_ARG, "hum_create: max_contacts out of range for the selected kernel");
     HIPCHK(hipSetDevice(cfg->device));
@@ -155,9 +165,12 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (st == hipSuccess) st = hipMalloc(&e->d.phys, HUM_NSTATE * n * e->real_size);
     if (st == hipSuccess) st = hipMalloc((void**)&e->d.bi, NBOOK_I * n * sizeof(int));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d.bd, NBOOK_D * n * sizeof(double));
-    if (st == hipSuccess)   // per-lane rows (kernel 0) or the per-env row spill region (kernel 1)
-        // (cooperative kernel: per-block regions, so round the lane count up to a multiple of 4 envs)
-        st = hipMalloc(&e->d.scratch, (size_t)(cfg->kernel == 1 ? GROW_PER_ENV * ((n + 3) / 4 * 4) : SCRATCH_PER_LANE * n) * e->real_size);
+    if (st == hipSuccess) {   // per-lane rows (kernel 0) or the per-block row spill regions (kernel 1)
+        const int epb = cfg->envs_per_block;
+        const size_t blocks = (n + epb - 1) / epb;
+        st = hipMalloc(&e->d.scratch, (cfg->kernel == 1 ? (size_t)grow_rows_per_block(epb, lds_rows_of(*cfg)) * RW * blocks
+                                                          : (size_t)SCRATCH_PER_LANE * n) * e->real_size);
+    }
     if (st == hipSuccess) st = hipMalloc((void**)&e->eflags, sizeof(unsigned));
     if (st == hipSuccess) st = hipMalloc((void**)&e->clips_dev, HUM_MAX_CLIPS * sizeof(ClipDev));
     if (st == hipSuccess) st = hipMemset(e->clips_dev, 0, HUM_MAX_CLIPS * sizeof(ClipDev));
@@ -568,11 +581,11 @@ int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
 
 #ifdef HUM_PHASE_TIMING
 // diagnostic builds only: accumulated s_memtime cycles per cooperative-kernel phase (thread 0 of each block)
-int hum_debug_phase_cycles(unsigned long long* out16, int reset) {
+int hum_debug_phase_cycles(unsigned long long* out32, int reset) {
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase_cycles), 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phase_cycles), 32 * sizeof(unsigned long long)));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[32] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
     }
     return HUM_OK;

@@ -580,6 +580,11 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     const int i = blockIdx.x * EPB_ + ge;
     const bool valid = i < a.n;
     GroupLDS<T>& S = sh[ge];
+#ifdef HUM_PHASE_TIMING
+    const unsigned long long t_wave0 = __builtin_amdgcn_s_memtime();
+#endif
+    load_tab_lds<T>();
+    __syncthreads();
     const ModelTab<T>& M = tab<T>();
     for (int e = l; e < HUM_NSTATE; e += GL)
         S.st[e] = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
@@ -599,7 +604,8 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++)
-            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * EPB_ * GROW_PER_ENV, l, ef);
+            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_rows_per_block(EPB_, a.P.lds_rows) * RW,
+                                   l, ef);
     }
     PHASE_INIT;
     if (valid && l == 0) {
@@ -628,6 +634,14 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
         }
     }
     PHASE(10);
+#ifdef HUM_PHASE_TIMING
+    if (threadIdx.x == 0) {   // wave duration: max (tail) and mean
+        const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t_wave0;
+        atomicMax(&g_phase_cycles[16], dtw);
+        atomicAdd(&g_phase_cycles[17], dtw);
+        atomicAdd(&g_phase_cycles[18], 1ull);
+    }
+#endif
     if (ef) atomicOr(a.eflags, ef);
 }
 

@@ -31,6 +31,7 @@ struct PhysParams {
     int max_contacts;
     int self_collision;
     int joint_damping;
+    int lds_rows;         // cooperative kernel: constraint rows per block kept in LDS (block row pool capacity)
 };
 
 constexpr int NV = 6 + NDOF;

@@ -92,11 +92,36 @@ constexpr ModelTab<T> make_tab() {
 static __constant__ ModelTab<float> kTabF = make_tab<float>();   // per translation unit
 static __constant__ ModelTab<double> kTabD = make_tab<double>();
 template <typename T> __device__ inline const ModelTab<T>& tab();
+#ifdef HUM_TAB_LDS
+// fp32: the cooperative kernel indexes the tables by lane (body, dof, geom, candidate), which from
+// __constant__ memory are per-lane vector-memory loads with L1/L2 latency on every dependent chain.  Each
+// block keeps its own 4.5 KB LDS copy instead, filled once per launch by load_tab_lds.
+static __shared__ ModelTab<float> sTabF;
+template <> __device__ inline const ModelTab<float>& tab<float>() { return sTabF; }
+#else
 template <> __device__ inline const ModelTab<float>& tab<float>() { return kTabF; }
+#endif
 template <> __device__ inline const ModelTab<double>& tab<double>() { return kTabD; }
 
-constexpr int MAXR_LDS = 30;                 // rows kept in LDS; rows beyond spill to a per-env global region
-constexpr int GROW_PER_ENV = (MAXR_G - MAXR_LDS) * RW;
+template <typename T>
+__device__ inline void load_tab_lds() {   // block-wide; the caller's __syncthreads publishes it
+#ifdef HUM_TAB_LDS
+    if constexpr (sizeof(T) == 4) {
+        static_assert(sizeof(ModelTab<float>) % 4 == 0, "word copy");
+        const int* src = reinterpret_cast<const int*>(&kTabF);
+        int* dst = reinterpret_cast<int*>(&sTabF);
+        for (int w = threadIdx.x; w < (int)(sizeof(ModelTab<float>) / 4); w += blockDim.x) dst[w] = src[w];
+    }
+#endif
+}
+
+// rows kept in LDS; rows beyond spill to a per-env global region and the wave takes the slow PGS path
+// (random-policy rollouts: p99 20 rows, > 30 in 0.04% of env-substeps; but the launch lasts as long as
+// its slowest wave, so a smaller capacity costs more than its frequency suggests: 24 rows is 9% slower)
+#ifndef HUM_MAXR_LDS
+#define HUM_MAXR_LDS 30
+#endif
+constexpr int MAXR_LDS = HUM_MAXR_LDS;
 
 template <typename T>
 struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront per SIMD
@@ -118,9 +143,22 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
     } x;
 };
 
+// ---- block row pool.  The rows of a block's EPB_ envs are packed back to back (env 0's, then env 1's, ...)
+// over its EPB_ * MAXR_LDS LDS row slots (slot s = row s % MAXR_LDS of env struct s / MAXR_LDS), so one env
+// may hold more than MAXR_LDS rows while the block total fits: the random-policy per-env tail (> 30 rows in
+// 0.04% of env-substeps) no longer sends a wave to the global spill path, which made it the launch's
+// slowest wave.  Positions from P.lds_rows on go to the block's global spill region (never observed with a
+// random policy; tests force it with hum_config.lds_rows).
+template <typename T>
+__device__ __attribute__((always_inline)) inline int pool_off(int p) {   // byte offset from the block's LDS array
+    const int s = p / MAXR_LDS, i = p - s * MAXR_LDS;
+    return s * (int)sizeof(GroupLDS<T>) + (int)offsetof(GroupLDS<T>, x.cr.row) + i * RW * (int)sizeof(T);
+}
+__host__ __device__ constexpr int grow_rows_per_block(int epb, int cap) { return epb * MAXR_G - cap; }
+
 // ---- diagnostic phase timing (compiled only with -DHUM_PHASE_TIMING; never in the shipped library)
 #ifdef HUM_PHASE_TIMING
-__device__ unsigned long long g_phase_cycles[16];
+__device__ unsigned long long g_phase_cycles[32];
 #define PHASE(k)                                                                 \
     do {                                                                         \
         if (threadIdx.x == 0) {                                                  \
@@ -382,12 +420,14 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
 // Row t of the wave's concatenated row list (env 0's rows, then env 1's, ...) goes to lane t % (16 EPB_):
 // per-env counts are wave-uniform (readlane), so the env/row of a task is two compares away.
 template <typename T>
-__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc, int nrm_off) {
+__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc, int next_off,
+                                                         int nrm_off) {
 #pragma unroll
     for (int q = 0; q < NV; q++) { R[q] = J[q]; R[NV + q] = Mi[q]; }
 #pragma unroll
-    for (int q = 0; q < 7; q++) R[2 * NV + q] = sc[q];
-    *reinterpret_cast<int*>(R + 2 * NV + 7) = nrm_off;   // slot 2NV+7 of a T row
+    for (int q = 0; q < 6; q++) R[2 * NV + q] = sc[q];
+    *reinterpret_cast<int*>(R + 2 * NV + 6) = next_off;   // int slots 2NV+6 / 2NV+7 of a T row
+    *reinterpret_cast<int*>(R + 2 * NV + 7) = nrm_off;
 }
 template <typename T>
 __device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J, const T* Mi, const T* sc) {
@@ -396,32 +436,40 @@ __device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J
 #pragma unroll
     for (int q = 0; q < NV; q++) { __builtin_nontemporal_store(J[q], R + q); __builtin_nontemporal_store(Mi[q], R + NV + q); }
 #pragma unroll
-    for (int q = 0; q < 7; q++) __builtin_nontemporal_store(sc[q], R + 2 * NV + q);
+    for (int q = 0; q < 6; q++) __builtin_nontemporal_store(sc[q], R + 2 * NV + q);
 }
 
 template <typename T, int EPB_>
-__device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, GroupLDS<T>* shb, T* grow_block, int nl, int nc,
-                                                          const T dt) {
+__device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, GroupLDS<T>* shb, T* gblock, int nl, int nc,
+                                                          const T dt, int& pbase, int& ptot) {
     const ModelTab<T>& M = tab<T>();
-    const int lane = threadIdx.x & 63;
-    int cnt[EPB_], nls[EPB_], ncs[EPB_], pre[EPB_ + 1];
+    const int lane = threadIdx.x & 63, cap = P.lds_rows;
+    // pre: task prefix (actual rows); pos: pool prefix (a single row is paired with a zero row, see PGS)
+    int cnt[EPB_], nls[EPB_], ncs[EPB_], pre[EPB_ + 1], pos[EPB_ + 1];
     pre[0] = 0;
+    pos[0] = 0;
 #pragma unroll
     for (int e = 0; e < EPB_; e++) {
         nls[e] = __builtin_amdgcn_readlane(nl, e * GL);
         ncs[e] = __builtin_amdgcn_readlane(nc, e * GL);
         cnt[e] = nls[e] + 3 * ncs[e];
         pre[e + 1] = pre[e] + cnt[e];
+        pos[e + 1] = pos[e] + (cnt[e] == 1 ? 2 : cnt[e]);
     }
+    pbase = 0;
+#pragma unroll
+    for (int q = 0; q < EPB_; q++)
+        if (q == lane / GL) pbase = pos[q];
+    ptot = pos[EPB_];
     const int total = pre[EPB_];
     for (int t = lane; t < total; t += EPB_ * GL) {
         int e = 0;
 #pragma unroll
         for (int q = 1; q < EPB_; q++) e += t >= pre[q] ? 1 : 0;
-        int r = t, enl = nls[0], enc = ncs[0];
+        int r = t, enl = nls[0], enc = ncs[0], epos = 0, ecnt = cnt[0];
 #pragma unroll
         for (int q = 0; q < EPB_; q++)
-            if (q == e) { r = t - pre[q]; enl = nls[q]; enc = ncs[q]; }
+            if (q == e) { r = t - pre[q]; enl = nls[q]; enc = ncs[q]; epos = pos[q]; ecnt = cnt[q]; }
         const GroupLDS<T>& S = shb[e];
         const auto& C = S.x.cr;
         // every row type (limit / normal / friction) funnels into ONE test-impulse response call: the wave's
@@ -491,16 +539,20 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         T jm = 0;
 #pragma unroll
         for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];   // limit rows: sg * Mi[6 + d] (sg^2 = 1)
-        sc[1] = 0;
+        sc[1] = 0;   // lo = 0 for every row type: the PGS reads this slot as its zero pad
         sc[3] = 0;
         sc[4] = T(1) / jm;
-        sc[6] = 0;
-        // PGS: byte offset (from row 0) of the lambda bounding this row - its normal row for a friction row,
-        // any row (row 0) otherwise (mu = 0 there)
-        const int nrm = r >= enl + enc ? (r + enl - enc) >> 1 : 0;
-        const int nrm_off = (nrm < MAXR_LDS ? nrm : 0) * RW * (int)sizeof(T) + (2 * NV + 3) * (int)sizeof(T);
-        if (r < MAXR_LDS) store_row(shb[e].x.cr.row[r], J, Mi, sc, nrm_off);
-        else store_row_global(grow_block + (long)e * GROW_PER_ENV + (r - MAXR_LDS) * RW, J, Mi, sc);
+        // PGS links (byte offsets from the block's LDS array, used only when the block's rows all fit in
+        // LDS): the env's next row in cyclic order, and the lambda bounding this row - its normal row's for
+        // a friction row, its own otherwise (mu = 0 there)
+        const int p = epos + r;
+        const int pn = epos + (r + 1 == (ecnt == 1 ? 2 : ecnt) ? 0 : r + 1);
+        const int pl = r >= enl + enc ? epos + ((r + enl - enc) >> 1) : p;
+        if (p < cap)
+            store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, pool_off<T>(pn),
+                      pool_off<T>(pl < cap ? pl : 0) + (2 * NV + 3) * (int)sizeof(T));
+        else
+            store_row_global(gblock + (long)(p - cap) * RW, J, Mi, sc);
     }
 }
 
@@ -667,9 +719,8 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
 template <typename T, int EPB_>
 __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>* shb, const int ge,
-                                                             T* grow_block, const int l, unsigned& ef) {
+                                                             T* gblock, const int l, unsigned& ef) {
     GroupLDS<T>& S = shb[ge];
-    T* grow = grow_block + (long)ge * GROW_PER_ENV;
     const ModelTab<T>& M = tab<T>();
     const T dt = (T)P.dt;
     PHASE_INIT;
@@ -985,41 +1036,55 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     // ---- rows (limits, normals, frictions): Jacobian + test-impulse response, one row per lane, the rows of
     //      all EPB_ envs of the wave spread over its lanes (one round instead of max_e ceil(nrows_e / 16))
     const int nrows = nl + 3 * nc;
-    group_rows<T, EPB_>(P, shb, grow_block, nl, nc, dt);
+    int pbase, ptot;   // this env's first pool position, the block's pool positions in use
+    group_rows<T, EPB_>(P, shb, gblock, nl, nc, dt, pbase, ptot);
+    const int cap = P.lds_rows;
     __syncthreads();
     PHASE(7);
     // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
     //      re-reads values it wrote itself, so no cross-lane LDS ordering is needed inside the loop.
     T n0 = S.nu[l], n1 = l < NV - GL ? S.nu[GL + l] : T(0);
+#ifdef HUM_PHASE_TIMING
+    {   // row statistics: slow-path waves, waves, rows per env, envs with > 24 / > 30 rows
+        const unsigned long long slow = ptot > cap;
+        if (threadIdx.x == 0) { atomicAdd(&g_phase_cycles[11], slow); atomicAdd(&g_phase_cycles[12], 1ull); }
+        if (l == 0) {
+            atomicAdd(&g_phase_cycles[13], (unsigned long long)nrows);
+            atomicAdd(&g_phase_cycles[14], (unsigned long long)(nrows > 24));
+            atomicAdd(&g_phase_cycles[15], (unsigned long long)(nrows > 30));
+        }
+    }
+#endif
 #ifndef HUM_PGS_SLOW
-    if (__ballot(nrows > MAXR_LDS || nrows == 1) == 0) {
+    if (ptot <= cap) {   // wave-uniform
 #else
     if (false) {
 #endif
-        // Common case (every env of the wave keeps >= 2 rows, all in LDS): software-pipelined over the
-        // flattened (iteration, row) sequence with ping-pong register sets - the next row's J / M^-1 J^T
-        // entries and scalars are read while the current row's 16-lane DPP reduction runs; the friction
-        // rows' normal lambda is read right after the previous row's lambda store (LDS ops of a wave are
-        // ordered), so it sees the update when that row was its normal.  Branch-free bounds: normal and
-        // limit rows store mu = 0, friction rows lo = hi = 0, so [lo - mu ln, hi + mu ln] is exact for all.
-        struct RowRegs { T j0, j1, m0, m1, b, lo, hi, lam, meff, mu; int nrm_off; };
-        const T* rowbase = &C.row[0][0];
-        // lanes without a second nu component read the row's zero pad: no branch or select on loaded values
-        const int lj1 = l < NV - GL ? GL + l : 2 * NV + 6, lm1 = l < NV - GL ? NV + GL + l : 2 * NV + 6;
+        // Common case (the block's rows all in its LDS pool): software-pipelined over the flattened
+        // (iteration, row) sequence with ping-pong register sets - the next row (linked by byte offset) is
+        // read while the current row's 16-lane DPP reduction runs; the friction rows' normal lambda is read
+        // right after the previous row's lambda store (LDS ops of a wave are ordered), so it sees the update
+        // when that row was its normal.  Branch-free bounds: every row has lo = 0, normal and limit rows
+        // store mu = 0, friction rows hi = 0, so [-mu ln, hi + mu ln] is exact for all.
+        struct RowRegs { T j0, j1, m0, m1, b, hi, lam, meff, mu; int next, nrm_off; };
+        const char* lds0 = reinterpret_cast<const char*>(shb);
+        // lanes without a second nu component read the row's lo slot (always 0): no branch or select
+        const int lj1 = l < NV - GL ? GL + l : 2 * NV + 1, lm1 = l < NV - GL ? NV + GL + l : 2 * NV + 1;
         auto load = [&](const T* R, RowRegs& d) {
             d.j0 = R[l];
             d.j1 = R[lj1];
             d.m0 = R[NV + l];
             d.m1 = R[lm1];
-            d.b = R[2 * NV + 0]; d.lo = R[2 * NV + 1]; d.hi = R[2 * NV + 2]; d.lam = R[2 * NV + 3];
+            d.b = R[2 * NV + 0]; d.hi = R[2 * NV + 2]; d.lam = R[2 * NV + 3];
             d.meff = R[2 * NV + 4]; d.mu = R[2 * NV + 5];
+            d.next = *reinterpret_cast<const int*>(R + 2 * NV + 6);
             d.nrm_off = *reinterpret_cast<const int*>(R + 2 * NV + 7);
         };
-        auto load_ln = [&](const RowRegs& d) -> T {   // normal lambda (byte offset precomputed per row)
-            return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(rowbase) + d.nrm_off);
+        auto load_ln = [&](const RowRegs& d) -> T {   // bounding lambda (byte offset precomputed per row)
+            return *reinterpret_cast<const T*>(lds0 + d.nrm_off);
         };
         auto update = [&](const RowRegs& d, T ln, T* R) {
-            const T lo = d.lo - d.mu * ln, hi = d.hi + d.mu * ln;
+            const T lo = -(d.mu * ln), hi = d.hi + d.mu * ln;
             const T jv = row_sum(d.j0 * n0 + d.j1 * n1);
             const T lnew = med3(d.lam + d.meff * (d.b - jv), lo, hi);   // == clamp: lo <= hi always
             R[2 * NV + 3] = lnew;
@@ -1027,33 +1092,43 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             n0 += d.m0 * dl;
             n1 += d.m1 * dl;
         };
-        const int total = P.iters * nrows;
+        // a single row would be its own successor (prefetched before its lambda store): pair it with a zero
+        // row (J = M^-1 J^T = b = bounds = lambda = 0, normal offset -> its own lambda): every update of it is
+        // lnew = 0, dl = 0, so the real row sees exactly its own P.iters updates in order
+        if (nrows == 1) {   // pool position pbase + 1 was reserved for it
+            const int zoff = pool_off<T>(pbase + 1);
+            T* Z = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + zoff);
+            Z[l] = T(0); Z[GL + l] = T(0); Z[2 * GL + l] = T(0);
+            if (l < 2 * NV + 6 - 3 * GL) Z[3 * GL + l] = T(0);
+            if (l == 0) *reinterpret_cast<int*>(Z + 2 * NV + 6) = pool_off<T>(pbase);
+            if (l == 1) *reinterpret_cast<int*>(Z + 2 * NV + 7) = zoff + (2 * NV + 3) * (int)sizeof(T);
+        }
+        wave_sync();
+        const int total = P.iters * (nrows == 1 ? 2 : nrows);
         if (total > 0) {
             RowRegs A, B;
-            const T* RA = rowbase;
+            const T* RA = reinterpret_cast<const T*>(lds0 + pool_off<T>(pbase));
             load(RA, A);
             T lnA = load_ln(A), lnB;
-            int r = 0;
             for (int k = 0;; k += 2) {
-                int rn = r + 1 == nrows ? 0 : r + 1;
-                const T* RB = rowbase + rn * RW;
+                const T* RB = reinterpret_cast<const T*>(lds0 + A.next);
                 load(RB, B);
                 update(A, lnA, const_cast<T*>(RA));
                 lnB = load_ln(B);
                 if (k + 1 >= total) break;
-                r = rn;
-                rn = r + 1 == nrows ? 0 : r + 1;
-                RA = rowbase + rn * RW;
+                RA = reinterpret_cast<const T*>(lds0 + B.next);
                 load(RA, A);
                 update(B, lnB, const_cast<T*>(RB));
                 lnA = load_ln(A);
                 if (k + 2 >= total) break;
-                r = rn;
             }
         }
     } else {
-        // some env spilled rows to its global region: plain loop with separately typed LDS / global rows
-        auto lam_of = [&](int r) -> T { return r < MAXR_LDS ? C.row[r][2 * NV + 3] : grow[(r - MAXR_LDS) * RW + 2 * NV + 3]; };
+        // the block's rows overflow its LDS pool: plain loop over pool positions (LDS or global spill region)
+        auto rowp = [&](int p) -> T* {
+            return p < cap ? reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)) : gblock + (long)(p - cap) * RW;
+        };
+        auto lam_of = [&](int r) -> T { return rowp(pbase + r)[2 * NV + 3]; };
         auto solve = [&](T* R, int r) {
             T lo = R[2 * NV + 1], hi = R[2 * NV + 2];
             if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
@@ -1072,11 +1147,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             n0 += m0 * dl;
             n1 += m1 * dl;
         };
-        for (int it = 0; it < P.iters; it++) {
-            const int nr_lds = nrows < MAXR_LDS ? nrows : MAXR_LDS;
-            for (int r = 0; r < nr_lds; r++) solve(C.row[r], r);
-            for (int r = MAXR_LDS; r < nrows; r++) solve(grow + (r - MAXR_LDS) * RW, r);
-        }
+        for (int it = 0; it < P.iters; it++)
+            for (int r = 0; r < nrows; r++) solve(rowp(pbase + r), r);
     }
     PHASE(8);
     S.nu[l] = n0;

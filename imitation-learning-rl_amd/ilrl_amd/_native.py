@@ -8,7 +8,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
-HUM_ABI_VERSION = 3   # include/humanoid_env.h
+HUM_ABI_VERSION = 4   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 12
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW = 1, 2
@@ -44,7 +44,7 @@ class HumConfig(ctypes.Structure):
                 ("limit_max_impulse", ctypes.c_double), ("max_coord_vel", ctypes.c_double),
                 ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
                 ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32),
-                ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32)]
+                ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32), ("lds_rows", ctypes.c_int32)]
 
 
 class NativeError(RuntimeError):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 3
+#define HUM_ABI_VERSION 4
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -119,6 +119,9 @@ typedef struct hum_config {
     int32_t envs_per_block;   /* cooperative kernel: envs per wavefront-block (4 = 64 threads (default), 2 = 32,
                                  1 = 16).  Fewer envs per wave buys SIMD co-residency but multiplies the wave
                                  instruction stream per env: measured 0.39 / 0.64 / 0.98 ms at 4096 envs */
+    int32_t lds_rows;         /* cooperative kernel: constraint rows per block kept in LDS; 0 (default) = the whole
+                                 pool (envs_per_block * 30), k > 0 caps it at k rows so the rest take the global
+                                 spill path (testing) */
 } hum_config;
 
 /* Version / build info. */

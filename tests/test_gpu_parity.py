@@ -61,9 +61,9 @@ def book_rows(r, t_idx):
     return out
 
 
-def run_scenario(r, precision, skip_physics, kernel=1):
+def run_scenario(r, precision, skip_physics, kernel=1, **physics):
     T = len(r["reward"])
-    env = HumanoidVecEnv(T, clips=(str(r["clip"]),), precision=precision, kernel=kernel)
+    env = HumanoidVecEnv(T, clips=(str(r["clip"]),), precision=precision, kernel=kernel, **physics)
     if len(r["predefined"]):
         env.set_predefined_targets(r["predefined"])
     phys = r["state_post"] if skip_physics else r["state_pre"]
@@ -127,6 +127,23 @@ def test_physics_fp64_matches_oracle(golden, name, kernel):
     np.testing.assert_array_equal(o["done"], r["done"])
     np.testing.assert_allclose(o["obs"], r["obs"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(o["rew"], r["reward"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("lds_rows", [1, 7])
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_physics_row_spill_path_matches_oracle(golden, precision, lds_rows):
+    """Cooperative kernel with its block row pool capped at lds_rows: the rows past the cap take the global
+    spill path of the PGS (1 = all but one row of every block, 7 = a mix of LDS and global rows)."""
+    errs = []
+    for name in scenarios(golden):
+        r = rec(golden, name)
+        o = run_scenario(r, precision, skip_physics=False, kernel=1, lds_rows=lds_rows)
+        if precision == "fp64":
+            err = np.abs(o["phys"] - r["state_post"])
+            assert err.max() < 1e-6, "%s: max state err %.3g" % (name, err.max())
+            np.testing.assert_array_equal(o["done"], r["done"])
+        errs.append(np.abs(o["obs"] - r["obs"]).max(axis=1))
+    assert np.median(np.concatenate(errs)) < 1e-3
 
 
 @pytest.mark.parametrize("kernel", [1, 0])
