@@ -579,6 +579,32 @@ int hum_sync(hum_env* e) {
 
 int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
 
+#ifdef HUM_CHECK_LINKS
+int hum_debug_check(unsigned* out8, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_check), 8 * sizeof(unsigned)));
+    if (reset) {
+        unsigned z[8] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_check), z, sizeof z));
+    }
+    return HUM_OK;
+}
+#endif
+
+#ifdef HUM_WLOG_ON
+int hum_debug_wave_log(unsigned* out, int nblocks, int reset) {   // diag: per-block work log (WLOG_W u32 each)
+    HIPCHK(hipDeviceSynchronize());
+    if (nblocks > 65536) nblocks = 65536;
+    if (out) HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_log), (size_t)nblocks * WLOG_W * sizeof(unsigned)));
+    if (reset) {
+        void* p = nullptr;
+        HIPCHK(hipGetSymbolAddress(&p, HIP_SYMBOL(g_wave_log)));
+        HIPCHK(hipMemset(p, 0, sizeof(g_wave_log)));
+    }
+    return HUM_OK;
+}
+#endif
+
 #ifdef HUM_PHASE_TIMING
 // diagnostic builds only: accumulated s_memtime cycles per cooperative-kernel phase (thread 0 of each block)
 int hum_debug_phase_cycles(unsigned long long* out32, int reset) {

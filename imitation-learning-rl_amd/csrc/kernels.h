@@ -580,8 +580,12 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     const int i = blockIdx.x * EPB_ + ge;
     const bool valid = i < a.n;
     GroupLDS<T>& S = sh[ge];
-#ifdef HUM_PHASE_TIMING
+#ifdef HUM_WLOG_ON
     const unsigned long long t_wave0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt_wave0 = __builtin_amdgcn_s_memrealtime();
+#ifdef HUM_WAVE_LOG
+    if (threadIdx.x < 12) s_phase[threadIdx.x] = 0;
+#endif
 #endif
     load_tab_lds<T>();
     __syncthreads();
@@ -634,12 +638,24 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
         }
     }
     PHASE(10);
-#ifdef HUM_PHASE_TIMING
+#ifdef HUM_WLOG_ON
     if (threadIdx.x == 0) {   // wave duration: max (tail) and mean
         const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t_wave0;
+#ifdef HUM_PHASE_TIMING
         atomicMax(&g_phase_cycles[16], dtw);
         atomicAdd(&g_phase_cycles[17], dtw);
         atomicAdd(&g_phase_cycles[18], 1ull);
+#endif
+        if (blockIdx.x < 65536) {
+            g_wave_log[blockIdx.x][0] = (unsigned)dtw;
+            g_wave_log[blockIdx.x][5] = (unsigned)rt_wave0;   // 100 MHz, device-wide
+            g_wave_log[blockIdx.x][4] = (unsigned)(__builtin_amdgcn_s_memrealtime() - rt_wave0);
+            g_wave_log[blockIdx.x][6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+            g_wave_log[blockIdx.x][7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+#ifdef HUM_WAVE_LOG
+            for (int k = 1; k <= 10; k++) g_wave_log[blockIdx.x][8 + k] = (unsigned)s_phase[k];
+#endif
+        }
     }
 #endif
     if (ef) atomicOr(a.eflags, ef);

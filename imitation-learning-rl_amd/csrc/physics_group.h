@@ -21,9 +21,16 @@ namespace hk {
 constexpr int GL = 16;                       // lanes per env
 constexpr int MAXC_G = 16;                   // contact cap of the cooperative kernel
 constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // 65 rows
-constexpr int RW = 2 * NV + 8;               // J[NV], M[NV], b, lo, hi, lam, meff, mu, 0 (pad read by lanes
-                                             // without a second nu component: branch-free PGS loads),
-                                             // byte offset of the friction row's normal lambda (int bits)
+// constraint row layout (T units): J and M^-1 J^T interleaved per dof ([2q] = J_q, [2q+1] = (M^-1 J^T)_q), a
+// zero pair (read by the lanes without a second velocity component), then two 16-byte scalar quads:
+// b, hi, lambda, 1/(J M^-1 J^T) and mu, c = J . (M^-1 J^T of the predecessor row), next3, next3_ln (ints).
+// lo is 0 for every row type and not stored.
+constexpr int RO_Z = 2 * NV;          // zero pair
+constexpr int RO_S0 = 2 * NV + 2;     // b, hi, lam, meff
+constexpr int RO_S1 = 2 * NV + 6;     // mu, c, next3, next3_ln
+constexpr int RO_LAM = RO_S0 + 2;
+constexpr int RW = 2 * NV + 10;
+static_assert(RO_S0 % 4 == 0 && RW % 4 == 0, "16-byte scalar quads");
 constexpr int NCAND_GROUND = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 1 : 2; return n; }();
 constexpr int NCAND = NCAND_GROUND + NPAIR;
 
@@ -137,7 +144,7 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
         struct {   // contacts + constraint rows
             T gp[NGEOM][2][3];
             T con[MAXC_G][12];
-            T row[MAXR_LDS][RW];
+            alignas(16) T row[MAXR_LDS][RW];
             int rdesc[MAXR_G];   // limit rows: dof | side << 8
         } cr;
     } x;
@@ -156,7 +163,31 @@ __device__ __attribute__((always_inline)) inline int pool_off(int p) {   // byte
 }
 __host__ __device__ constexpr int grow_rows_per_block(int epb, int cap) { return epb * MAXR_G - cap; }
 
-// ---- diagnostic phase timing (compiled only with -DHUM_PHASE_TIMING; never in the shipped library)
+// ---- diagnostics (never in the shipped library): -DHUM_PHASE_TIMING = per-phase s_memtime counters (global
+// atomics: they slow the kernel and skew it between XCDs) + the per-block work log; -DHUM_WAVE_LOG = the work
+// log alone (one plain store per block at its end: timing close to the shipped kernel)
+#if defined(HUM_PHASE_TIMING) || defined(HUM_WAVE_LOG)
+#define HUM_WLOG_ON 1
+// per-block work log: [0] s_memtime duration, [1] PGS length, [2] row rounds, [3] narrow-phase rounds,
+// [4] s_memrealtime duration, [5] s_memrealtime start, [6] HW_ID, [7] XCC_ID, [8 + k] phase k cycles
+// (HUM_WAVE_LOG builds: accumulated in LDS by thread 0, written at the end)
+constexpr int WLOG_W = 20;
+__device__ unsigned g_wave_log[65536][WLOG_W];
+template <int EPB_>
+__device__ inline int env_max(int x) {   // max over the wave's envs of a per-env (group-uniform) value
+    int m = __builtin_amdgcn_readlane(x, 0);
+#pragma unroll
+    for (int e = 1; e < EPB_; e++) m = max(m, __builtin_amdgcn_readlane(x, e * 16));
+    return m;
+}
+#define WLOG(k, v)                                                               \
+    do {                                                                         \
+        const int v_ = (v);                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 65536) g_wave_log[blockIdx.x][k] += v_; \
+    } while (0)
+#else
+#define WLOG(k, v) do { } while (0)
+#endif
 #ifdef HUM_PHASE_TIMING
 __device__ unsigned long long g_phase_cycles[32];
 #define PHASE(k)                                                                 \
@@ -164,6 +195,17 @@ __device__ unsigned long long g_phase_cycles[32];
         if (threadIdx.x == 0) {                                                  \
             unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
             atomicAdd(&g_phase_cycles[k], t_ - t_last_);                         \
+            t_last_ = t_;                                                        \
+        }                                                                        \
+    } while (0)
+#define PHASE_INIT unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
+#elif defined(HUM_WAVE_LOG)
+static __shared__ unsigned long long s_phase[12];
+#define PHASE(k)                                                                 \
+    do {                                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
+            s_phase[k] += t_ - t_last_;                                          \
             t_last_ = t_;                                                        \
         }                                                                        \
     } while (0)
@@ -176,6 +218,9 @@ __device__ unsigned long long g_phase_cycles[32];
 #define PHASE_INIT do { } while (0)
 #endif
 
+#ifdef HUM_CHECK_LINKS
+__device__ unsigned g_check[8];
+#endif
 __device__ inline void wave_sync() {   // cross-lane LDS ordering inside one wavefront
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -420,23 +465,48 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
 // Row t of the wave's concatenated row list (env 0's rows, then env 1's, ...) goes to lane t % (16 EPB_):
 // per-env counts are wave-uniform (readlane), so the env/row of a task is two compares away.
 template <typename T>
-__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc, int next_off,
-                                                         int nrm_off) {
+__device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc, int next3,
+                                                         int next3_ln) {
 #pragma unroll
-    for (int q = 0; q < NV; q++) { R[q] = J[q]; R[NV + q] = Mi[q]; }
-#pragma unroll
-    for (int q = 0; q < 6; q++) R[2 * NV + q] = sc[q];
-    *reinterpret_cast<int*>(R + 2 * NV + 6) = next_off;   // int slots 2NV+6 / 2NV+7 of a T row
-    *reinterpret_cast<int*>(R + 2 * NV + 7) = nrm_off;
+    for (int q = 0; q < NV; q++) { R[2 * q] = J[q]; R[2 * q + 1] = Mi[q]; }
+    R[RO_Z] = T(0); R[RO_Z + 1] = T(0);
+    R[RO_S0] = sc[0]; R[RO_S0 + 1] = sc[2]; R[RO_S0 + 2] = sc[3]; R[RO_S0 + 3] = sc[4];
+    R[RO_S1] = sc[5]; R[RO_S1 + 1] = T(0);   // c: filled by group_couplings
+    *reinterpret_cast<int*>(R + RO_S1 + 2) = next3;
+    *reinterpret_cast<int*>(R + RO_S1 + 3) = next3_ln;
 }
 template <typename T>
 __device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J, const T* Mi, const T* sc) {
     // spilled rows: nontemporal stores keep the compiler from merging this path with the LDS one into
     // generic (flat) stores
 #pragma unroll
-    for (int q = 0; q < NV; q++) { __builtin_nontemporal_store(J[q], R + q); __builtin_nontemporal_store(Mi[q], R + NV + q); }
-#pragma unroll
-    for (int q = 0; q < 6; q++) __builtin_nontemporal_store(sc[q], R + 2 * NV + q);
+    for (int q = 0; q < NV; q++) { __builtin_nontemporal_store(J[q], R + 2 * q); __builtin_nontemporal_store(Mi[q], R + 2 * q + 1); }
+    __builtin_nontemporal_store(sc[0], R + RO_S0);
+    __builtin_nontemporal_store(sc[2], R + RO_S0 + 1);
+    __builtin_nontemporal_store(sc[3], R + RO_S0 + 2);
+    __builtin_nontemporal_store(sc[4], R + RO_S0 + 3);
+    __builtin_nontemporal_store(sc[5], R + RO_S1);
+}
+
+// PGS pool count of an env with n rows: 0, or at least PGS_AHEAD + 1 (zero rows pad it, see the PGS)
+constexpr int PGS_AHEAD = 3;   // the PGS reads row k + PGS_AHEAD while row k is solved
+__device__ inline int pool_rows(int n) { return n == 0 ? 0 : (n < PGS_AHEAD + 1 ? PGS_AHEAD + 1 : n); }
+// PGS links (byte offsets from the block's LDS array, used only when the block's rows all fit in LDS) of
+// row r of an env (pool rows from epos, neff = pool_rows(ecnt) of them, ecnt real rows: enl limits, enc
+// normals, 2 enc frictions): the row PGS_AHEAD ahead in cyclic order, and the lambda bounding it - its
+// normal row's for a friction row, its own otherwise (mu = 0 there).  The PGS reads that row while row r is
+// solved, so rows r..r+2 are not yet updated: bits 0 / 1 / 2 of the lambda offset flag a normal row that is
+// row r + 2 / r + 1 / r, whose fresh lambda the PGS forwards from registers.
+template <typename T>
+__device__ inline void pgs_link(int epos, int r, int ecnt, int enl, int enc, int& next3, int& next3_ln) {
+    static_assert(RO_LAM * sizeof(T) % 8 == 0 && RW * sizeof(T) % 16 == 0, "flag bits of the lambda offsets");
+    const int neff = pool_rows(ecnt);
+    const int rs = (r + PGS_AHEAD) % neff;
+    const bool sfric = rs >= enl + enc && rs < ecnt;
+    const int nrm_s = enl + ((rs - enl - enc) >> 1);
+    const int fwd = sfric ? (nrm_s == (r + 2) % neff ? 1 : 0) | (nrm_s == (r + 1) % neff ? 2 : 0) | (nrm_s == r ? 4 : 0) : 0;
+    next3 = pool_off<T>(epos + rs);
+    next3_ln = (pool_off<T>(epos + (sfric ? nrm_s : rs)) + RO_LAM * (int)sizeof(T)) | fwd;
 }
 
 template <typename T, int EPB_>
@@ -444,7 +514,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                                                           const T dt, int& pbase, int& ptot) {
     const ModelTab<T>& M = tab<T>();
     const int lane = threadIdx.x & 63, cap = P.lds_rows;
-    // pre: task prefix (actual rows); pos: pool prefix (a single row is paired with a zero row, see PGS)
+    // pre: task prefix (actual rows); pos: pool prefix (short envs are padded with zero rows, see PGS)
     int cnt[EPB_], nls[EPB_], ncs[EPB_], pre[EPB_ + 1], pos[EPB_ + 1];
     pre[0] = 0;
     pos[0] = 0;
@@ -454,7 +524,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         ncs[e] = __builtin_amdgcn_readlane(nc, e * GL);
         cnt[e] = nls[e] + 3 * ncs[e];
         pre[e + 1] = pre[e] + cnt[e];
-        pos[e + 1] = pos[e] + (cnt[e] == 1 ? 2 : cnt[e]);
+        pos[e + 1] = pos[e] + pool_rows(cnt[e]);
     }
     pbase = 0;
 #pragma unroll
@@ -462,6 +532,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         if (q == lane / GL) pbase = pos[q];
     ptot = pos[EPB_];
     const int total = pre[EPB_];
+    WLOG(2, (total + EPB_ * GL - 1) / (EPB_ * GL));
     for (int t = lane; t < total; t += EPB_ * GL) {
         int e = 0;
 #pragma unroll
@@ -480,6 +551,9 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         const bool lim = r < enl;
         if (lim) {
             const int d = C.rdesc[r] & 0xff, side = C.rdesc[r] >> 8;
+#ifdef HUM_CHECK_LINKS
+            if (d >= NDOF || side > 1) atomicAdd(&g_check[5], 1u);
+#endif
             const T sg = side == 0 ? T(1) : T(-1);
             const T q = S.st[13 + d];
             const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
@@ -542,17 +616,38 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         sc[1] = 0;   // lo = 0 for every row type: the PGS reads this slot as its zero pad
         sc[3] = 0;
         sc[4] = T(1) / jm;
-        // PGS links (byte offsets from the block's LDS array, used only when the block's rows all fit in
-        // LDS): the env's next row in cyclic order, and the lambda bounding this row - its normal row's for
-        // a friction row, its own otherwise (mu = 0 there)
         const int p = epos + r;
-        const int pn = epos + (r + 1 == (ecnt == 1 ? 2 : ecnt) ? 0 : r + 1);
-        const int pl = r >= enl + enc ? epos + ((r + enl - enc) >> 1) : p;
-        if (p < cap)
-            store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, pool_off<T>(pn),
-                      pool_off<T>(pl < cap ? pl : 0) + (2 * NV + 3) * (int)sizeof(T));
-        else
+        if (p < cap) {
+            int n3, n3ln;
+            pgs_link<T>(epos, r, ecnt, enl, enc, n3, n3ln);   // (used only when all of the block's rows are in LDS)
+            store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, n3, n3ln);
+        }
+        else {
             store_row_global(gblock + (long)(p - cap) * RW, J, Mi, sc);
+        }
+    }
+    // couplings c_r = J_r . (M^-1 J^T)_pred(r) (cyclic predecessor; 0 after a zero row) for the lookahead
+    // PGS, which needs them only when the block's rows all sit in LDS
+    if (pos[EPB_] <= cap) {
+        wave_sync();
+        for (int t = lane; t < total; t += EPB_ * GL) {
+            int e = 0;
+#pragma unroll
+            for (int q = 1; q < EPB_; q++) e += t >= pre[q] ? 1 : 0;
+            int r = t, epos = 0, ecnt = cnt[0];
+#pragma unroll
+            for (int q = 0; q < EPB_; q++)
+                if (q == e) { r = t - pre[q]; epos = pos[q]; ecnt = cnt[q]; }
+            const int rp = r == 0 ? pool_rows(ecnt) - 1 : r - 1;
+            if (rp < ecnt) {
+                T* Rr = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(epos + r));
+                const T* Rp = reinterpret_cast<const T*>(reinterpret_cast<const char*>(shb) + pool_off<T>(epos + rp));
+                T c = 0;
+#pragma unroll
+                for (int q = 0; q < NV; q++) c += Rr[2 * q] * Rp[2 * q + 1];
+                Rr[RO_S1 + 1] = c;
+            }
+        }
     }
 }
 
@@ -998,6 +1093,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             ns += __popcll(bm);
         }
         wave_sync();
+        WLOG(3, (env_max<EPB_>(ns) + GL - 1) / GL);
         for (int r0 = 0; r0 < ns; r0 += GL) {
             const int j = r0 + l;
             bool hit = false;
@@ -1005,6 +1101,9 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             T pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
             if (j < ns) {
                 const int k = surv[j];
+#ifdef HUM_CHECK_LINKS
+                if ((unsigned)k >= (unsigned)NPAIR) atomicAdd(&g_check[4], 1u);
+#endif
                 const int ga = M.cand_a[NCAND_GROUND + k], gb = M.cand_b[NCAND_GROUND + k];
                 T ca[3], cb[3], dv[3];
                 seg_seg(C.gp[ga][0], C.gp[ga][1], C.gp[gb][0], C.gp[gb][1], ca, cb);
@@ -1039,6 +1138,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     int pbase, ptot;   // this env's first pool position, the block's pool positions in use
     group_rows<T, EPB_>(P, shb, gblock, nl, nc, dt, pbase, ptot);
     const int cap = P.lds_rows;
+    WLOG(1, env_max<EPB_>(nrows));
     __syncthreads();
     PHASE(7);
     // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
@@ -1060,67 +1160,111 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #else
     if (false) {
 #endif
-        // Common case (the block's rows all in its LDS pool): software-pipelined over the flattened
-        // (iteration, row) sequence with ping-pong register sets - the next row (linked by byte offset) is
-        // read while the current row's 16-lane DPP reduction runs; the friction rows' normal lambda is read
-        // right after the previous row's lambda store (LDS ops of a wave are ordered), so it sees the update
-        // when that row was its normal.  Branch-free bounds: every row has lo = 0, normal and limit rows
-        // store mu = 0, friction rows hi = 0, so [-mu ln, hi + mu ln] is exact for all.
-        struct RowRegs { T j0, j1, m0, m1, b, hi, lam, meff, mu; int next, nrm_off; };
+        // Common case (the block's rows all in its LDS pool).  Gauss-Seidel over the flattened (iteration,
+        // row) sequence, restated for latency: with n_k the velocity before row k and dl_k its impulse change,
+        //     J_k . n_k = J_k . n_(k-1) + dl_(k-1) c_k,    c_k = J_k . M^-1 J_(k-1)^T (precomputed per row),
+        // so the 16-lane reduction of J_k . n_(k-1) runs while row k-1 is solved, and the row-to-row
+        // dependency chain is 5 scalar ops (fma, sub, fma, med3, sub).  Row k+3 is read while row k is solved
+        // (through a link stored in row k), two stages before its reduction needs it; the lambdas it reads were
+        // stored earlier (LDS ops of a wave are ordered) except a bounding lambda of rows k..k+2, forwarded from
+        // registers, and pool_rows pads an env to >= 4 rows so a row is never re-read before its own store.
+        // Branch-free bounds: lo = 0 for every row, normal and limit rows have mu = 0, friction rows hi = 0,
+        // so [-mu ln, hi + mu ln] is exact for all.
+        using T2 = typename std::conditional<sizeof(T) == 4, float2, double2>::type;
+        struct RowRegs { T j0, m0, j1, m1, b, hi, lam, meff, mu, c; int next3, next3_ln; };
         const char* lds0 = reinterpret_cast<const char*>(shb);
-        // lanes without a second nu component read the row's lo slot (always 0): no branch or select
-        const int lj1 = l < NV - GL ? GL + l : 2 * NV + 1, lm1 = l < NV - GL ? NV + GL + l : 2 * NV + 1;
-        auto load = [&](const T* R, RowRegs& d) {
-            d.j0 = R[l];
-            d.j1 = R[lj1];
-            d.m0 = R[NV + l];
-            d.m1 = R[lm1];
-            d.b = R[2 * NV + 0]; d.hi = R[2 * NV + 2]; d.lam = R[2 * NV + 3];
-            d.meff = R[2 * NV + 4]; d.mu = R[2 * NV + 5];
-            d.next = *reinterpret_cast<const int*>(R + 2 * NV + 6);
-            d.nrm_off = *reinterpret_cast<const int*>(R + 2 * NV + 7);
+        const int off0 = 2 * l * (int)sizeof(T), off1 = (l < NV - GL ? 2 * (GL + l) : RO_Z) * (int)sizeof(T);
+        auto as_int = [](T v) -> int {
+            if constexpr (sizeof(T) == 4) return __float_as_int(v);
+            else return (int)(unsigned)__double_as_longlong(v);
         };
-        auto load_ln = [&](const RowRegs& d) -> T {   // bounding lambda (byte offset precomputed per row)
-            return *reinterpret_cast<const T*>(lds0 + d.nrm_off);
+        auto load = [&](int off, RowRegs& d) {
+            const char* R = lds0 + off;
+            const T2 p0 = *reinterpret_cast<const T2*>(R + off0), p1 = *reinterpret_cast<const T2*>(R + off1);
+            d.j0 = p0.x; d.m0 = p0.y; d.j1 = p1.x; d.m1 = p1.y;
+            if constexpr (sizeof(T) == 4) {
+                const float4 s0 = *reinterpret_cast<const float4*>(R + RO_S0 * sizeof(T));
+                const float4 s1 = *reinterpret_cast<const float4*>(R + RO_S1 * sizeof(T));
+                d.b = s0.x; d.hi = s0.y; d.lam = s0.z; d.meff = s0.w;
+                d.mu = s1.x; d.c = s1.y; d.next3 = __float_as_int(s1.z); d.next3_ln = __float_as_int(s1.w);
+            } else {
+                const T* S0 = reinterpret_cast<const T*>(R) + RO_S0;
+                d.b = S0[0]; d.hi = S0[1]; d.lam = S0[2]; d.meff = S0[3];
+                d.mu = S0[4]; d.c = S0[5]; d.next3 = as_int(S0[6]); d.next3_ln = as_int(S0[7]);
+            }
         };
-        auto update = [&](const RowRegs& d, T ln, T* R) {
-            const T lo = -(d.mu * ln), hi = d.hi + d.mu * ln;
-            const T jv = row_sum(d.j0 * n0 + d.j1 * n1);
-            const T lnew = med3(d.lam + d.meff * (d.b - jv), lo, hi);   // == clamp: lo <= hi always
-            R[2 * NV + 3] = lnew;
-            const T dl = lnew - d.lam;
-            n0 += d.m0 * dl;
-            n1 += d.m1 * dl;
-        };
-        // a single row would be its own successor (prefetched before its lambda store): pair it with a zero
-        // row (J = M^-1 J^T = b = bounds = lambda = 0, normal offset -> its own lambda): every update of it is
-        // lnew = 0, dl = 0, so the real row sees exactly its own P.iters updates in order
-        if (nrows == 1) {   // pool position pbase + 1 was reserved for it
-            const int zoff = pool_off<T>(pbase + 1);
-            T* Z = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + zoff);
-            Z[l] = T(0); Z[GL + l] = T(0); Z[2 * GL + l] = T(0);
-            if (l < 2 * NV + 6 - 3 * GL) Z[3 * GL + l] = T(0);
-            if (l == 0) *reinterpret_cast<int*>(Z + 2 * NV + 6) = pool_off<T>(pbase);
-            if (l == 1) *reinterpret_cast<int*>(Z + 2 * NV + 7) = zoff + (2 * NV + 3) * (int)sizeof(T);
+        auto load_ln = [&](int ln_off) -> T { return *reinterpret_cast<const T*>(lds0 + (ln_off & ~7)); };
+        const int neff = pool_rows(nrows);
+        // zero rows pad short envs (pool positions reserved by group_rows): J = M^-1 J^T = b = bounds =
+        // lambda = c = 0, so each of their updates is lnew = 0, dl = 0
+        if (nrows > 0 && nrows < neff) {
+            for (int z = nrows; z < neff; z++) {
+                T* Z = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(pbase + z));
+                int n3, n3ln;
+                pgs_link<T>(pbase, z, nrows, nl, nc, n3, n3ln);
+                Z[l] = T(0); Z[GL + l] = T(0); Z[2 * GL + l] = T(0);
+                if (l < RW - 2 - 3 * GL) Z[3 * GL + l] = T(0);
+                if (l == 0) *reinterpret_cast<int*>(Z + RO_S1 + 2) = n3;
+                if (l == 1) *reinterpret_cast<int*>(Z + RO_S1 + 3) = n3ln;
+            }
         }
         wave_sync();
-        const int total = P.iters * (nrows == 1 ? 2 : nrows);
+        const int total = P.iters * neff;
+#ifdef HUM_CHECK_LINKS
+        // diagnostic: every link of the env's cycle is what pgs_link says
+        if (l == 0 && total > 0) {
+            for (int r = 0; r < neff; r++) {
+                const char* R = lds0 + pool_off<T>(pbase + r);
+                int e3, e3ln;
+                pgs_link<T>(pbase, r, nrows, nl, nc, e3, e3ln);
+                if (*reinterpret_cast<const int*>(R + (RO_S1 + 2) * sizeof(T)) != e3) atomicAdd(&g_check[0], 1u);
+                if (*reinterpret_cast<const int*>(R + (RO_S1 + 3) * sizeof(T)) != e3ln) atomicAdd(&g_check[1], 1u);
+            }
+            if (pbase + neff > ptot || ptot > cap) atomicAdd(&g_check[2], 1u);
+            atomicAdd(&g_check[3], 1u);
+        }
+#endif
         if (total > 0) {
-            RowRegs A, B;
-            const T* RA = reinterpret_cast<const T*>(lds0 + pool_off<T>(pbase));
-            load(RA, A);
-            T lnA = load_ln(A), lnB;
-            for (int k = 0;; k += 2) {
-                const T* RB = reinterpret_cast<const T*>(lds0 + A.next);
-                load(RB, B);
-                update(A, lnA, const_cast<T*>(RA));
-                lnB = load_ln(B);
+            RowRegs A, B, C, D;
+            int oA = pool_off<T>(pbase), oB = pool_off<T>(pbase + 1), oC = pool_off<T>(pbase + 2), oD;
+            load(oA, A);
+            load(oB, B);
+            load(oC, C);
+            // rows 1 and 2: links from rows neff-2 and neff-1 (their forward flags can only name rows 0 / 1)
+            auto link_ln = [&](int r) { return *reinterpret_cast<const int*>(lds0 + pool_off<T>(pbase + r) + (RO_S1 + 3) * sizeof(T)); };
+            const int ln1 = link_ln(neff - 2), ln2 = link_ln(neff - 1);
+            int fA = 0, fB = ln1 & 7, fC = ln2 & 7, fD;
+            T lnA = T(0), lnB = load_ln(ln1), lnC = load_ln(ln2), lnD;   // the first row is a limit or normal row (mu = 0)
+            T sA = row_sum(A.j0 * n0 + A.j1 * n1), sB, sC, sD, dlp = T(0);
+            // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read
+            auto stage = [&](const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX, T& sY, T lnX, T& lnY,
+                             T& lnZ, T& lnW, int fY, int fZ, int& fW) {
+                oW = X.next3;
+                fW = X.next3_ln & 7;
+                load(oW, W);
+                lnW = load_ln(X.next3_ln);
+                sY = row_sum(Y.j0 * n0 + Y.j1 * n1);
+                const T jv = sX + dlp * X.c;
+                const T lo = -(X.mu * lnX), hi = X.hi + X.mu * lnX;
+                const T lnew = med3(X.lam + X.meff * (X.b - jv), lo, hi);   // == clamp: lo <= hi always
+                *reinterpret_cast<T*>(const_cast<char*>(lds0) + oX + RO_LAM * sizeof(T)) = lnew;
+                const T dl = lnew - X.lam;
+                n0 += X.m0 * dl;
+                n1 += X.m1 * dl;
+                dlp = dl;
+                if (fY & 1) lnY = lnew;   // row k+1's normal row is row k
+                if (fZ & 2) lnZ = lnew;   // row k+2's
+                if (fW & 4) lnW = lnew;   // row k+3's
+            };
+            for (int k = 0;; k += 4) {
+                stage(A, B, D, oA, oD, sA, sB, lnA, lnB, lnC, lnD, fB, fC, fD);
                 if (k + 1 >= total) break;
-                RA = reinterpret_cast<const T*>(lds0 + B.next);
-                load(RA, A);
-                update(B, lnB, const_cast<T*>(RB));
-                lnA = load_ln(A);
+                stage(B, C, A, oB, oA, sB, sC, lnB, lnC, lnD, lnA, fC, fD, fA);
                 if (k + 2 >= total) break;
+                stage(C, D, B, oC, oB, sC, sD, lnC, lnD, lnA, lnB, fD, fA, fB);
+                if (k + 3 >= total) break;
+                stage(D, A, C, oD, oC, sD, sA, lnD, lnA, lnB, lnC, fA, fB, fC);
+                if (k + 4 >= total) break;
             }
         }
     } else {
@@ -1128,22 +1272,22 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         auto rowp = [&](int p) -> T* {
             return p < cap ? reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)) : gblock + (long)(p - cap) * RW;
         };
-        auto lam_of = [&](int r) -> T { return rowp(pbase + r)[2 * NV + 3]; };
+        auto lam_of = [&](int r) -> T { return rowp(pbase + r)[RO_LAM]; };
         auto solve = [&](T* R, int r) {
-            T lo = R[2 * NV + 1], hi = R[2 * NV + 2];
+            T lo = T(0), hi = R[RO_S0 + 1];
             if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
-                const T mu = R[2 * NV + 5];
+                const T mu = R[RO_S1];
                 const T ln = lam_of(nl + ((r - nl - nc) >> 1));
                 lo = -mu * ln;
                 hi = mu * ln;
             }
-            const T part = R[l] * n0 + (l < NV - GL ? R[GL + l] * n1 : T(0));
-            const T m0 = R[NV + l], m1 = l < NV - GL ? R[NV + GL + l] : T(0);
+            const T part = R[2 * l] * n0 + (l < NV - GL ? R[2 * (GL + l)] * n1 : T(0));
+            const T m0 = R[2 * l + 1], m1 = l < NV - GL ? R[2 * (GL + l) + 1] : T(0);
             const T jv = row_sum(part);
-            const T lam = R[2 * NV + 3];
-            const T lnew = clampT(lam + R[2 * NV + 4] * (R[2 * NV + 0] - jv), lo, hi);
+            const T lam = R[RO_LAM];
+            const T lnew = clampT(lam + R[RO_S0 + 3] * (R[RO_S0] - jv), lo, hi);
             const T dl = lnew - lam;
-            R[2 * NV + 3] = lnew;
+            R[RO_LAM] = lnew;
             n0 += m0 * dl;
             n1 += m1 * dl;
         };

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B throughput of experiment libraries: bench each libhumenv_{fast,v*}.so, two alternating passes
 cd "$GRAFT_REPO_ROOT" || exit 1
+shopt -s nullglob
 mkdir -p gpurun_out
 L=$PWD/imitation-learning-rl_amd/ilrl_amd/_lib
 for pass in 1 2; do
