@@ -488,9 +488,9 @@ __device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J
     __builtin_nontemporal_store(sc[5], R + RO_S1);
 }
 
-// PGS pool count of an env with n rows: 0, or at least PGS_AHEAD + 1 (zero rows pad it, see the PGS)
+// PGS pool count of an env with n rows: at least PGS_AHEAD + 1 (zero rows pad it, see the PGS)
 constexpr int PGS_AHEAD = 3;   // the PGS reads row k + PGS_AHEAD while row k is solved
-__device__ inline int pool_rows(int n) { return n == 0 ? 0 : (n < PGS_AHEAD + 1 ? PGS_AHEAD + 1 : n); }
+__device__ inline int pool_rows(int n) { return n < PGS_AHEAD + 1 ? PGS_AHEAD + 1 : n; }
 // PGS links (byte offsets from the block's LDS array, used only when the block's rows all fit in LDS) of
 // row r of an env (pool rows from epos, neff = pool_rows(ecnt) of them, ecnt real rows: enl limits, enc
 // normals, 2 enc frictions): the row PGS_AHEAD ahead in cyclic order, and the lambda bounding it - its
@@ -1197,7 +1197,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         const int neff = pool_rows(nrows);
         // zero rows pad short envs (pool positions reserved by group_rows): J = M^-1 J^T = b = bounds =
         // lambda = c = 0, so each of their updates is lnew = 0, dl = 0
-        if (nrows > 0 && nrows < neff) {
+        if (nrows < neff) {
             for (int z = nrows; z < neff; z++) {
                 T* Z = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(pbase + z));
                 int n3, n3ln;
@@ -1212,7 +1212,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         const int total = P.iters * neff;
 #ifdef HUM_CHECK_LINKS
         // diagnostic: every link of the env's cycle is what pgs_link says
-        if (l == 0 && total > 0) {
+        if (l == 0) {
             for (int r = 0; r < neff; r++) {
                 const char* R = lds0 + pool_off<T>(pbase + r);
                 int e3, e3ln;
@@ -1224,7 +1224,12 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             atomicAdd(&g_check[3], 1u);
         }
 #endif
-        if (total > 0) {
+        {
+            // one wave-uniform trip count (the longest env's, in whole rounds of 4 stages): an env past its
+            // own count keeps cycling its rows with updates masked to dl = 0, so the loop has no divergent exits
+            int tmax = total;
+#pragma unroll
+            for (int e = 0; e < EPB_; e++) tmax = max(tmax, __builtin_amdgcn_readlane(total, e * GL));
             RowRegs A, B, C, D;
             int oA = pool_off<T>(pbase), oB = pool_off<T>(pbase + 1), oC = pool_off<T>(pbase + 2), oD;
             load(oA, A);
@@ -1237,8 +1242,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             T lnA = T(0), lnB = load_ln(ln1), lnC = load_ln(ln2), lnD;   // the first row is a limit or normal row (mu = 0)
             T sA = row_sum(A.j0 * n0 + A.j1 * n1), sB, sC, sD, dlp = T(0);
             // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read
-            auto stage = [&](const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX, T& sY, T lnX, T& lnY,
-                             T& lnZ, T& lnW, int fY, int fZ, int& fW) {
+            auto stage = [&](int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX, T& sY, T lnX,
+                             T& lnY, T& lnZ, T& lnW, int fY, int fZ, int& fW) {
                 oW = X.next3;
                 fW = X.next3_ln & 7;
                 load(oW, W);
@@ -1246,7 +1251,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 sY = row_sum(Y.j0 * n0 + Y.j1 * n1);
                 const T jv = sX + dlp * X.c;
                 const T lo = -(X.mu * lnX), hi = X.hi + X.mu * lnX;
-                const T lnew = med3(X.lam + X.meff * (X.b - jv), lo, hi);   // == clamp: lo <= hi always
+                const T lsol = med3(X.lam + X.meff * (X.b - jv), lo, hi);   // == clamp: lo <= hi always
+                const T lnew = kk < total ? lsol : X.lam;
                 *reinterpret_cast<T*>(const_cast<char*>(lds0) + oX + RO_LAM * sizeof(T)) = lnew;
                 const T dl = lnew - X.lam;
                 n0 += X.m0 * dl;
@@ -1256,15 +1262,11 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 if (fZ & 2) lnZ = lnew;   // row k+2's
                 if (fW & 4) lnW = lnew;   // row k+3's
             };
-            for (int k = 0;; k += 4) {
-                stage(A, B, D, oA, oD, sA, sB, lnA, lnB, lnC, lnD, fB, fC, fD);
-                if (k + 1 >= total) break;
-                stage(B, C, A, oB, oA, sB, sC, lnB, lnC, lnD, lnA, fC, fD, fA);
-                if (k + 2 >= total) break;
-                stage(C, D, B, oC, oB, sC, sD, lnC, lnD, lnA, lnB, fD, fA, fB);
-                if (k + 3 >= total) break;
-                stage(D, A, C, oD, oC, sD, sA, lnD, lnA, lnB, lnC, fA, fB, fC);
-                if (k + 4 >= total) break;
+            for (int k = 0; k < tmax; k += 4) {
+                stage(k, A, B, D, oA, oD, sA, sB, lnA, lnB, lnC, lnD, fB, fC, fD);
+                stage(k + 1, B, C, A, oB, oA, sB, sC, lnB, lnC, lnD, lnA, fC, fD, fA);
+                stage(k + 2, C, D, B, oC, oB, sC, sD, lnC, lnD, lnA, lnB, fD, fA, fB);
+                stage(k + 3, D, A, C, oD, oC, sD, sA, lnD, lnA, lnB, lnC, fA, fB, fC);
             }
         }
     } else {
