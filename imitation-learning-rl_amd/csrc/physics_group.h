@@ -488,25 +488,32 @@ __device__ __attribute__((always_inline)) void store_row_global(T* R, const T* J
     __builtin_nontemporal_store(sc[5], R + RO_S1);
 }
 
-// PGS pool count of an env with n rows: at least PGS_AHEAD + 1 (zero rows pad it, see the PGS)
-constexpr int PGS_AHEAD = 3;   // the PGS reads row k + PGS_AHEAD while row k is solved
-__device__ inline int pool_rows(int n) { return n < PGS_AHEAD + 1 ? PGS_AHEAD + 1 : n; }
+// PGS pool layout of an env with nl limit rows and nc contacts (rows: limits, normals, 2 frictions per
+// contact): zero rows (J = M^-1 J^T = b = bounds = lambda = c = 0: every update of one is lnew = dl = 0)
+// between the normals and the frictions put each friction row at least PGS_AHEAD + 1 positions after its
+// normal row, and trail the cycle up to PGS_AHEAD + 1 positions.  The PGS reads the row PGS_AHEAD ahead (and
+// the lambda bounding it) while a row is solved, so every lambda it reads was stored before.
+constexpr int PGS_AHEAD = 3;
+__device__ inline int pool_gap(int nc) { return nc > 0 && nc < PGS_AHEAD + 1 ? PGS_AHEAD + 1 - nc : 0; }
+__device__ inline int pool_used(int nl, int nc) { return nl + 3 * nc + pool_gap(nc); }
+__device__ inline int pool_rows(int nl, int nc) {
+    const int u = pool_used(nl, nc);
+    return u < PGS_AHEAD + 1 ? PGS_AHEAD + 1 : u;
+}
+__device__ inline int pool_pos(int r, int nl, int nc) { return r < nl + nc ? r : r + pool_gap(nc); }   // real row r
+__device__ inline bool pool_zero(int q, int nl, int nc) {   // position q holds a zero row
+    return (q >= nl + nc && q < nl + nc + pool_gap(nc)) || q >= pool_used(nl, nc);
+}
 // PGS links (byte offsets from the block's LDS array, used only when the block's rows all fit in LDS) of
-// row r of an env (pool rows from epos, neff = pool_rows(ecnt) of them, ecnt real rows: enl limits, enc
-// normals, 2 enc frictions): the row PGS_AHEAD ahead in cyclic order, and the lambda bounding it - its
-// normal row's for a friction row, its own otherwise (mu = 0 there).  The PGS reads that row while row r is
-// solved, so rows r..r+2 are not yet updated: bits 0 / 1 / 2 of the lambda offset flag a normal row that is
-// row r + 2 / r + 1 / r, whose fresh lambda the PGS forwards from registers.
+// pool position q of an env: the position PGS_AHEAD ahead in cyclic order, and the lambda bounding it - its
+// normal row's for a friction row, its own otherwise (mu = 0 there)
 template <typename T>
-__device__ inline void pgs_link(int epos, int r, int ecnt, int enl, int enc, int& next3, int& next3_ln) {
-    static_assert(RO_LAM * sizeof(T) % 8 == 0 && RW * sizeof(T) % 16 == 0, "flag bits of the lambda offsets");
-    const int neff = pool_rows(ecnt);
-    const int rs = (r + PGS_AHEAD) % neff;
-    const bool sfric = rs >= enl + enc && rs < ecnt;
-    const int nrm_s = enl + ((rs - enl - enc) >> 1);
-    const int fwd = sfric ? (nrm_s == (r + 2) % neff ? 1 : 0) | (nrm_s == (r + 1) % neff ? 2 : 0) | (nrm_s == r ? 4 : 0) : 0;
-    next3 = pool_off<T>(epos + rs);
-    next3_ln = (pool_off<T>(epos + (sfric ? nrm_s : rs)) + RO_LAM * (int)sizeof(T)) | fwd;
+__device__ inline void pgs_link(int epos, int q, int nl, int nc, int& next3, int& next3_ln) {
+    const int neff = pool_rows(nl, nc), f0 = nl + nc + pool_gap(nc);
+    const int t = (q + PGS_AHEAD) % neff;
+    const bool fric = t >= f0 && t < pool_used(nl, nc);
+    next3 = pool_off<T>(epos + t);
+    next3_ln = pool_off<T>(epos + (fric ? nl + ((t - f0) >> 1) : t)) + RO_LAM * (int)sizeof(T);
 }
 
 template <typename T, int EPB_>
@@ -524,7 +531,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         ncs[e] = __builtin_amdgcn_readlane(nc, e * GL);
         cnt[e] = nls[e] + 3 * ncs[e];
         pre[e + 1] = pre[e] + cnt[e];
-        pos[e + 1] = pos[e] + pool_rows(cnt[e]);
+        pos[e + 1] = pos[e] + pool_rows(nls[e], ncs[e]);
     }
     pbase = 0;
 #pragma unroll
@@ -537,10 +544,10 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         int e = 0;
 #pragma unroll
         for (int q = 1; q < EPB_; q++) e += t >= pre[q] ? 1 : 0;
-        int r = t, enl = nls[0], enc = ncs[0], epos = 0, ecnt = cnt[0];
+        int r = t, enl = nls[0], enc = ncs[0], epos = 0;
 #pragma unroll
         for (int q = 0; q < EPB_; q++)
-            if (q == e) { r = t - pre[q]; enl = nls[q]; enc = ncs[q]; epos = pos[q]; ecnt = cnt[q]; }
+            if (q == e) { r = t - pre[q]; enl = nls[q]; enc = ncs[q]; epos = pos[q]; }
         const GroupLDS<T>& S = shb[e];
         const auto& C = S.x.cr;
         // every row type (limit / normal / friction) funnels into ONE test-impulse response call: the wave's
@@ -616,10 +623,10 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         sc[1] = 0;   // lo = 0 for every row type: the PGS reads this slot as its zero pad
         sc[3] = 0;
         sc[4] = T(1) / jm;
-        const int p = epos + r;
+        const int p = epos + pool_pos(r, enl, enc);
         if (p < cap) {
             int n3, n3ln;
-            pgs_link<T>(epos, r, ecnt, enl, enc, n3, n3ln);   // (used only when all of the block's rows are in LDS)
+            pgs_link<T>(epos, p - epos, enl, enc, n3, n3ln);   // (used only when all of the block's rows are in LDS)
             store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, n3, n3ln);
         }
         else {
@@ -634,14 +641,15 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             int e = 0;
 #pragma unroll
             for (int q = 1; q < EPB_; q++) e += t >= pre[q] ? 1 : 0;
-            int r = t, epos = 0, ecnt = cnt[0];
+            int r = t, epos = 0, enl = nls[0], enc = ncs[0];
 #pragma unroll
             for (int q = 0; q < EPB_; q++)
-                if (q == e) { r = t - pre[q]; epos = pos[q]; ecnt = cnt[q]; }
-            const int rp = r == 0 ? pool_rows(ecnt) - 1 : r - 1;
-            if (rp < ecnt) {
-                T* Rr = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(epos + r));
-                const T* Rp = reinterpret_cast<const T*>(reinterpret_cast<const char*>(shb) + pool_off<T>(epos + rp));
+                if (q == e) { r = t - pre[q]; epos = pos[q]; enl = nls[q]; enc = ncs[q]; }
+            const int qr = pool_pos(r, enl, enc);
+            const int qp = qr == 0 ? pool_rows(enl, enc) - 1 : qr - 1;
+            if (!pool_zero(qp, enl, enc)) {
+                T* Rr = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(epos + qr));
+                const T* Rp = reinterpret_cast<const T*>(reinterpret_cast<const char*>(shb) + pool_off<T>(epos + qp));
                 T c = 0;
 #pragma unroll
                 for (int q = 0; q < NV; q++) c += Rr[2 * q] * Rp[2 * q + 1];
@@ -1166,8 +1174,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         // so the 16-lane reduction of J_k . n_(k-1) runs while row k-1 is solved, and the row-to-row
         // dependency chain is 5 scalar ops (fma, sub, fma, med3, sub).  Row k+3 is read while row k is solved
         // (through a link stored in row k), two stages before its reduction needs it; the lambdas it reads were
-        // stored earlier (LDS ops of a wave are ordered) except a bounding lambda of rows k..k+2, forwarded from
-        // registers, and pool_rows pads an env to >= 4 rows so a row is never re-read before its own store.
+        // stored earlier (LDS ops of a wave are ordered: the pool layout keeps a friction row >= 4 positions
+        // after its normal row and a cycle >= 4 positions long, see pool_gap).
         // Branch-free bounds: lo = 0 for every row, normal and limit rows have mu = 0, friction rows hi = 0,
         // so [-mu ln, hi + mu ln] is exact for all.
         using T2 = typename std::conditional<sizeof(T) == 4, float2, double2>::type;
@@ -1193,15 +1201,14 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 d.mu = S0[4]; d.c = S0[5]; d.next3 = as_int(S0[6]); d.next3_ln = as_int(S0[7]);
             }
         };
-        auto load_ln = [&](int ln_off) -> T { return *reinterpret_cast<const T*>(lds0 + (ln_off & ~7)); };
-        const int neff = pool_rows(nrows);
-        // zero rows pad short envs (pool positions reserved by group_rows): J = M^-1 J^T = b = bounds =
-        // lambda = c = 0, so each of their updates is lnew = 0, dl = 0
-        if (nrows < neff) {
-            for (int z = nrows; z < neff; z++) {
+        auto load_ln = [&](int ln_off) -> T { return *reinterpret_cast<const T*>(lds0 + ln_off); };
+        const int neff = pool_rows(nl, nc);
+        // the zero rows of the pool layout (positions reserved by group_rows)
+        for (int z = nl + nc; z < neff; z++) {
+            if (pool_zero(z, nl, nc)) {
                 T* Z = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(pbase + z));
                 int n3, n3ln;
-                pgs_link<T>(pbase, z, nrows, nl, nc, n3, n3ln);
+                pgs_link<T>(pbase, z, nl, nc, n3, n3ln);
                 Z[l] = T(0); Z[GL + l] = T(0); Z[2 * GL + l] = T(0);
                 if (l < RW - 2 - 3 * GL) Z[3 * GL + l] = T(0);
                 if (l == 0) *reinterpret_cast<int*>(Z + RO_S1 + 2) = n3;
@@ -1216,7 +1223,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (int r = 0; r < neff; r++) {
                 const char* R = lds0 + pool_off<T>(pbase + r);
                 int e3, e3ln;
-                pgs_link<T>(pbase, r, nrows, nl, nc, e3, e3ln);
+                pgs_link<T>(pbase, r, nl, nc, e3, e3ln);
                 if (*reinterpret_cast<const int*>(R + (RO_S1 + 2) * sizeof(T)) != e3) atomicAdd(&g_check[0], 1u);
                 if (*reinterpret_cast<const int*>(R + (RO_S1 + 3) * sizeof(T)) != e3ln) atomicAdd(&g_check[1], 1u);
             }
@@ -1235,17 +1242,13 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             load(oA, A);
             load(oB, B);
             load(oC, C);
-            // rows 1 and 2: links from rows neff-2 and neff-1 (their forward flags can only name rows 0 / 1)
-            auto link_ln = [&](int r) { return *reinterpret_cast<const int*>(lds0 + pool_off<T>(pbase + r) + (RO_S1 + 3) * sizeof(T)); };
-            const int ln1 = link_ln(neff - 2), ln2 = link_ln(neff - 1);
-            int fA = 0, fB = ln1 & 7, fC = ln2 & 7, fD;
-            T lnA = T(0), lnB = load_ln(ln1), lnC = load_ln(ln2), lnD;   // the first row is a limit or normal row (mu = 0)
+            // positions 0..2 are never friction rows (mu = 0): their bounds need no lambda
+            T lnA = T(0), lnB = T(0), lnC = T(0), lnD;
             T sA = row_sum(A.j0 * n0 + A.j1 * n1), sB, sC, sD, dlp = T(0);
             // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read
             auto stage = [&](int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX, T& sY, T lnX,
-                             T& lnY, T& lnZ, T& lnW, int fY, int fZ, int& fW) {
+                             T& lnW) {
                 oW = X.next3;
-                fW = X.next3_ln & 7;
                 load(oW, W);
                 lnW = load_ln(X.next3_ln);
                 sY = row_sum(Y.j0 * n0 + Y.j1 * n1);
@@ -1258,15 +1261,12 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 n0 += X.m0 * dl;
                 n1 += X.m1 * dl;
                 dlp = dl;
-                if (fY & 1) lnY = lnew;   // row k+1's normal row is row k
-                if (fZ & 2) lnZ = lnew;   // row k+2's
-                if (fW & 4) lnW = lnew;   // row k+3's
             };
             for (int k = 0; k < tmax; k += 4) {
-                stage(k, A, B, D, oA, oD, sA, sB, lnA, lnB, lnC, lnD, fB, fC, fD);
-                stage(k + 1, B, C, A, oB, oA, sB, sC, lnB, lnC, lnD, lnA, fC, fD, fA);
-                stage(k + 2, C, D, B, oC, oB, sC, sD, lnC, lnD, lnA, lnB, fD, fA, fB);
-                stage(k + 3, D, A, C, oD, oC, sD, sA, lnD, lnA, lnB, lnC, fA, fB, fC);
+                stage(k, A, B, D, oA, oD, sA, sB, lnA, lnD);
+                stage(k + 1, B, C, A, oB, oA, sB, sC, lnB, lnA);
+                stage(k + 2, C, D, B, oC, oB, sC, sD, lnC, lnB);
+                stage(k + 3, D, A, C, oD, oC, sD, sA, lnD, lnC);
             }
         }
     } else {
@@ -1274,7 +1274,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         auto rowp = [&](int p) -> T* {
             return p < cap ? reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)) : gblock + (long)(p - cap) * RW;
         };
-        auto lam_of = [&](int r) -> T { return rowp(pbase + r)[RO_LAM]; };
+        auto lam_of = [&](int r) -> T { return rowp(pbase + pool_pos(r, nl, nc))[RO_LAM]; };
         auto solve = [&](T* R, int r) {
             T lo = T(0), hi = R[RO_S0 + 1];
             if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
@@ -1294,7 +1294,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             n1 += m1 * dl;
         };
         for (int it = 0; it < P.iters; it++)
-            for (int r = 0; r < nrows; r++) solve(rowp(pbase + r), r);
+            for (int r = 0; r < nrows; r++) solve(rowp(pbase + pool_pos(r, nl, nc)), r);
     }
     PHASE(8);
     S.nu[l] = n0;
