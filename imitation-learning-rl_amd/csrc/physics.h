@@ -159,6 +159,37 @@ __device__ inline void forward_kinematics(const T* quat, const T* q, Kin<T>& K) 
     }
 }
 
+// the same with the hinge angles' sin / cos precomputed (scs[2d] = sin q_d, scs[2d+1] = cos q_d)
+template <typename T>
+__device__ inline void forward_kinematics_pre(const T* quat, const T* scs, Kin<T>& K) {
+    quat_to_mat(quat, K.R[0]);
+    K.o[0][0] = K.o[0][1] = K.o[0][2] = 0;
+#pragma unroll
+    for (int b = 1; b < NB; b++) {
+        const int p = body_parent[b];
+        T M[9];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                M[3 * r + c] = K.R[p][3 * r] * (T)body_Roff[9 * b + c] + K.R[p][3 * r + 1] * (T)body_Roff[9 * b + 3 + c] +
+                               K.R[p][3 * r + 2] * (T)body_Roff[9 * b + 6 + c];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+            K.o[b][i] = K.o[p][i] + K.R[p][3 * i] * (T)body_toff[3 * b] + K.R[p][3 * i + 1] * (T)body_toff[3 * b + 1] +
+                        K.R[p][3 * i + 2] * (T)body_toff[3 * b + 2];
+#pragma unroll
+        for (int k = 0; k < body_ndof[b]; k++) {
+            const int d = body_dof0[b] + k, ax = dof_axis[d];
+            const T sg = (T)dof_sign[d];
+            K.u[d][0] = M[ax] * sg; K.u[d][1] = M[3 + ax] * sg; K.u[d][2] = M[6 + ax] * sg;
+            rot_post(M, ax, scs[2 * d + 1], sg * scs[2 * d]);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; i++) K.R[b][i] = M[i];
+    }
+}
+
 // motion subspace column of dof d (body b) at the common origin: [u; o_b x u]
 template <typename T>
 __device__ inline void motion_col(const Kin<T>& K, int b, int d, T* S) {

@@ -126,7 +126,7 @@ __device__ inline void load_tab_lds() {   // block-wide; the caller's __syncthre
 // (random-policy rollouts: p99 20 rows, > 30 in 0.04% of env-substeps; but the launch lasts as long as
 // its slowest wave, so a smaller capacity costs more than its frequency suggests: 24 rows is 9% slower)
 #ifndef HUM_MAXR_LDS
-#define HUM_MAXR_LDS 30
+#define HUM_MAXR_LDS 29
 #endif
 constexpr int MAXR_LDS = HUM_MAXR_LDS;
 
@@ -135,7 +135,7 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
     T st[HUM_NSTATE + 1];
     T tau[NDOF + 3];
     T nu[NV + 1];
-    T R[NB][9], o[NB][3], u[NDOF][3];
+    T R[NB][9], o[NB][3], Sc[NDOF][6];   // Sc: motion subspace column [u; o x u] of each hinge (world axes)
     T U[NDOF][6], Dinv[NB][9], L0[21];
     union {
         struct {   // articulated-body pass (dead once the accelerations are known)
@@ -149,6 +149,12 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
         } cr;
     } x;
 };
+
+template <typename T>
+__device__ __attribute__((always_inline)) inline void load_sc(const GroupLDS<T>& S, int d, T* Sc) {
+#pragma unroll
+    for (int e = 0; e < 6; e++) Sc[e] = S.Sc[d][e];
+}
 
 // ---- block row pool.  The rows of a block's EPB_ envs are packed back to back (env 0's, then env 1's, ...)
 // over its EPB_ * MAXR_LDS LDS row slots (slot s = row s % MAXR_LDS of env struct s / MAXR_LDS), so one env
@@ -309,8 +315,8 @@ __device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int
 #pragma unroll
         for (int j = 0; j < k; j++) {
             const int d = d0 + j;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[b], S.u[d], Sc + 3);
+            T Sc[6];
+            load_sc(S, d, Sc);
             T s = (d == jd) ? jsign : T(0);
 #pragma unroll
             for (int e = 0; e < 6; e++) s -= Sc[e] * pA[b][e];
@@ -363,8 +369,8 @@ __device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int
             for (int j = 0; j < k; j++) s += S.Dinv[b][3 * i + j] * r[j];
             out[6 + d0 + i] = s;
             const int d = d0 + i;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[b], S.u[d], Sc + 3);
+            T Sc[6];
+            load_sc(S, d, Sc);
 #pragma unroll
             for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * s;
         }
@@ -383,8 +389,8 @@ __device__ inline void g_row_jacobian(const GroupLDS<T>& S, int b, const T* f, T
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[x], S.u[d], Sc + 3);
+            T Sc[6];
+            load_sc(S, d, Sc);
             T s = 0;
 #pragma unroll
             for (int e = 0; e < 6; e++) s += f[e] * Sc[e];
@@ -406,8 +412,8 @@ __device__ inline void g_row_jacobian2(const GroupLDS<T>& S, int ba, const T* fa
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[x], S.u[d], Sc + 3);
+            T Sc[6];
+            load_sc(S, d, Sc);
             T sa = 0, sb = 0;
 #pragma unroll
             for (int e = 0; e < 6; e++) { sa += fa[e] * Sc[e]; sb += fb[e] * Sc[e]; }
@@ -429,8 +435,8 @@ __device__ inline void g_body_vel2(const GroupLDS<T>& S, int ba, int bb, T* Va, 
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[x], S.u[d], Sc + 3);
+            T Sc[6];
+            load_sc(S, d, Sc);
             const T qd = S.nu[6 + d];
             const T qa = ona ? qd : T(0), qb = onb ? qd : T(0);
 #pragma unroll
@@ -451,8 +457,8 @@ __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
-            T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-            cross3(S.o[x], S.u[d], Sc + 3);
+            T Sc[6];
+            load_sc(S, d, Sc);
             const T qd = S.nu[6 + d];
             if (on)
 #pragma unroll
@@ -695,14 +701,13 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
         add_kid(g == 0 ? LVL_KID[LV][0][0] : (g == 1 ? LVL_KID[LV][1][0] : (g == 2 ? LVL_KID[LV][2][0] : LVL_KID[LV][3][0])));
     if constexpr (LVL_KID[LV][0][1] >= 0)
         add_kid(g == 0 ? LVL_KID[LV][0][1] : (g == 1 ? LVL_KID[LV][1][1] : (g == 2 ? LVL_KID[LV][2][1] : LVL_KID[LV][3][1])));
-    const T ob[3] = {S.o[b][0], S.o[b][1], S.o[b][2]};
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const bool on = j < k;
         const int d = on ? d0 + j : d0;
-        const T u[3] = {S.u[d][0], S.u[d][1], S.u[d][2]};
-        Sc[j][0] = on ? u[0] : T(0); Sc[j][1] = on ? u[1] : T(0); Sc[j][2] = on ? u[2] : T(0);
-        cross3(ob, Sc[j], Sc[j] + 3);
+        load_sc(S, d, Sc[j]);
+#pragma unroll
+        for (int e = 0; e < 6; e++) Sc[j][e] = on ? Sc[j][e] : T(0);
         symmv(IA, Sc[j], U[j]);
         T sp = 0;
 #pragma unroll
@@ -799,15 +804,14 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
         for (int e = 0; e < 6; e++) t -= S.U[d][e] * ap[e];
         r[j] = j < k ? t : T(0);
     }
-    const T ob[3] = {S.o[b][0], S.o[b][1], S.o[b][2]};
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         T t = 0;
 #pragma unroll
         for (int j = 0; j < 3; j++) t += S.Dinv[b][3 * i + j] * r[j];   // padded block: identity, r = 0
         const int d = i < k ? d0 + i : d0;
-        T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-        cross3(ob, Sc, Sc + 3);
+        T Sc[6];
+        load_sc(S, d, Sc);
         const T qdd = i < k ? t : T(0);
 #pragma unroll
         for (int e = 0; e < 6; e++) ab[e] += Sc[e] * qdd;
@@ -829,11 +833,21 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     PHASE_INIT;
     // ---- FK (every lane, registers); lane 0 publishes
     {
-        T st[HUM_NSTATE];
+        // the 17 hinge angles' sin / cos once, one per lane (scratch: the ABA transients are dead until pass 1)
+        T* scs = &S.x.aba.IA[0][0];
+        for (int d = l; d < NDOF; d += GL) {
+            T sn, cs;
+            if constexpr (sizeof(T) == 4) sincosf(S.st[13 + d], &sn, &cs);
+            else sincos(S.st[13 + d], &sn, &cs);
+            scs[2 * d] = sn;
+            scs[2 * d + 1] = cs;
+        }
+        wave_sync();
+        T quat[4];
 #pragma unroll
-        for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
+        for (int e = 0; e < 4; e++) quat[e] = S.st[3 + e];
         Kin<T> K;
-        forward_kinematics(st + 3, st + 13, K);
+        forward_kinematics_pre(quat, scs, K);
         if (l == 0) {
 #pragma unroll
             for (int b = 0; b < NB; b++) {
@@ -843,9 +857,14 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 for (int i = 0; i < 3; i++) S.o[b][i] = K.o[b][i];
             }
 #pragma unroll
-            for (int d = 0; d < NDOF; d++)
+            for (int b = 1; b < NB; b++)
 #pragma unroll
-                for (int i = 0; i < 3; i++) S.u[d][i] = K.u[d][i];
+                for (int k = 0; k < body_ndof[b]; k++) {   // motion subspace columns [u; o_b x u]
+                    const int d = body_dof0[b] + k;
+#pragma unroll
+                    for (int i = 0; i < 3; i++) S.Sc[d][i] = K.u[d][i];
+                    cross3(K.o[b], K.u[d], S.Sc[d] + 3);
+                }
         }
         if (l < 16) {   // generalised velocity
             S.nu[l] = l < 3 ? S.st[10 + l] : (l < 6 ? S.st[7 + l - 3] : S.st[30 + l - 6]);
@@ -867,8 +886,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #pragma unroll
             for (int k = 0; k < body_ndof[x]; k++) {
                 const int d = body_dof0[x] + k;
-                T Sc[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0};
-                cross3(S.o[x], S.u[d], Sc + 3);
+                T Sc[6];
+                load_sc(S, d, Sc);
                 if (on)
 #pragma unroll
                     for (int e = 0; e < 6; e++) V[e] += Sc[e] * S.nu[6 + d];
@@ -878,8 +897,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         const int k = M.ndof[b], d0 = M.dof0[b];
         for (int j = 0; j < k; j++) {
             const int d = d0 + j;
-            T Sq[6] = {S.u[d][0], S.u[d][1], S.u[d][2], 0, 0, 0}, cr[6];
-            cross3(S.o[b], S.u[d], Sq + 3);
+            T Sq[6], cr[6];
+            load_sc(S, d, Sq);
             const T qd = S.nu[6 + d];
 #pragma unroll
             for (int e = 0; e < 6; e++) { Sq[e] *= qd; V[e] += Sq[e]; }
