@@ -51,6 +51,20 @@ struct ModelTab {
     float act_gain[NACT];
 };
 
+// ONX[x] bit b: body x is body b or one of its ancestors (x >= 1).  Indexed by the compile-time x of an
+// unrolled loop and shifted by the lane-varying b, so "is x on b's path" costs one shift and no memory load
+// (a lane-varying table lookup is a vector-memory load with its full latency on the dependency chain).
+constexpr unsigned onx_mask(int x) {
+    unsigned m = 0;
+    for (int b = 0; b < NB; b++)
+        for (int y = b; y > 0; y = body_parent[y])
+            if (y == x) m |= 1u << b;
+    return m;
+}
+__device__ inline bool on_path(int x, int b) {   // b < 0: no body
+    return b >= 0 && ((onx_mask(x) >> (b & 31)) & 1u);
+}
+
 constexpr double csqrt(double x) {   // constexpr Newton square root (model constants only)
     if (x <= 0) return 0;
     double r = x > 1 ? x : 1;
@@ -380,12 +394,11 @@ __device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int
 // J row for a spatial force f on body b (generic: runtime b)
 template <typename T>
 __device__ inline void g_row_jacobian(const GroupLDS<T>& S, int b, const T* f, T sgn, T* J) {
-    const ModelTab<T>& M = tab<T>();
 #pragma unroll
     for (int e = 0; e < 6; e++) J[e] += sgn * f[e];
 #pragma unroll
     for (int x = 1; x < NB; x++) {
-        const bool on = b >= 0 && M.onpath[b < 0 ? 0 : b][x];
+        const bool on = on_path(x, b);
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
@@ -402,13 +415,12 @@ __device__ inline void g_row_jacobian(const GroupLDS<T>& S, int b, const T* f, T
 // J row for spatial forces fa on body ba and fb on body bb (either < 0 = absent), one pass over the dofs
 template <typename T>
 __device__ inline void g_row_jacobian2(const GroupLDS<T>& S, int ba, const T* fa, int bb, const T* fb, T* J) {
-    const ModelTab<T>& M = tab<T>();
 #pragma unroll
     for (int e = 0; e < 6; e++) J[e] = (ba >= 0 ? fa[e] : T(0)) + (bb >= 0 ? fb[e] : T(0));
 #pragma unroll
     for (int x = 1; x < NB; x++) {
-        const bool ona = ba >= 0 && M.onpath[ba < 0 ? 0 : ba][x];
-        const bool onb = bb >= 0 && M.onpath[bb < 0 ? 0 : bb][x];
+        const bool ona = on_path(x, ba);
+        const bool onb = on_path(x, bb);
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
@@ -425,13 +437,12 @@ __device__ inline void g_row_jacobian2(const GroupLDS<T>& S, int ba, const T* fa
 // spatial velocities of bodies ba and bb (bb < 0: Vb = 0) from nu, one pass over the dofs
 template <typename T>
 __device__ inline void g_body_vel2(const GroupLDS<T>& S, int ba, int bb, T* Va, T* Vb) {
-    const ModelTab<T>& M = tab<T>();
 #pragma unroll
     for (int e = 0; e < 6; e++) { Va[e] = S.nu[e]; Vb[e] = bb >= 0 ? S.nu[e] : T(0); }
 #pragma unroll
     for (int x = 1; x < NB; x++) {
-        const bool ona = ba >= 0 && M.onpath[ba < 0 ? 0 : ba][x];
-        const bool onb = bb >= 0 && M.onpath[bb < 0 ? 0 : bb][x];
+        const bool ona = on_path(x, ba);
+        const bool onb = on_path(x, bb);
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
@@ -448,12 +459,11 @@ __device__ inline void g_body_vel2(const GroupLDS<T>& S, int ba, int bb, T* Va, 
 // spatial velocity of body b from the generalised velocity nu (LDS)
 template <typename T>
 __device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
-    const ModelTab<T>& M = tab<T>();
 #pragma unroll
     for (int e = 0; e < 6; e++) V[e] = S.nu[e];
 #pragma unroll
     for (int x = 1; x < NB; x++) {
-        const bool on = b >= 0 && M.onpath[b < 0 ? 0 : b][x];
+        const bool on = on_path(x, b);
 #pragma unroll
         for (int k = 0; k < body_ndof[x]; k++) {
             const int d = body_dof0[x] + k;
@@ -882,7 +892,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         // parent velocity: path excluding b itself
 #pragma unroll
         for (int x = 1; x < NB; x++) {
-            const bool on = M.onpath[b][x] && x != b;
+            const bool on = on_path(x, b) && x != b;
 #pragma unroll
             for (int k = 0; k < body_ndof[x]; k++) {
                 const int d = body_dof0[x] + k;
