@@ -34,22 +34,23 @@ static_assert(RO_S0 % 4 == 0 && RW % 4 == 0, "16-byte scalar quads");
 constexpr int NCAND_GROUND = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 1 : 2; return n; }();
 constexpr int NCAND = NCAND_GROUND + NPAIR;
 
-// generic (runtime-indexable) model tables in __constant__ memory
+// the model tables the cooperative kernel indexes by lane-varying body / dof / link / geom / candidate
+// (compile-time-indexed constants come from model_gen.h directly)
 template <typename T>
 struct ModelTab {
-    int parent[NB], dof0[NB], ndof[NB], nlink[NB], link0[NB];
-    T toff[NB][3], Roff[NB][9], mass[NB], com[NB][3], inertia[NB][9];
-    int onpath[NB][NB];          // onpath[b][x]: x is b or an ancestor of b (x >= 1)
-    int daxis[NDOF];
-    T dsign[NDOF], lo[NDOF], hi[NDOF], damp[NDOF];
+    int dof0[NB], ndof[NB], nlink[NB], link0[NB];
+    T mass[NB], com[NB][3], inertia[NB][9];
+    T lo[NDOF], hi[NDOF], damp[NDOF];
     T lmass[NLINK], lcom[NLINK][3], linertia[NLINK][9];
-    int gbody[NGEOM], gtype[NGEOM];
+    int gbody[NGEOM];
     T gr[NGEOM], gp1[NGEOM][3], gp2[NGEOM][3];
-    int cand_a[NCAND], cand_b[NCAND];    // ground: (geom, endpoint) with cand_b = -1 - endpoint; pair: (ga, gb)
+    int cand[NCAND];                     // a | b << 16; ground: (geom, -1 - endpoint), pair: (ga, gb)
     T gbr[NGEOM];                        // bounding-sphere radius about the segment midpoint: |p2-p1|/2 + r
     int act_dof[NACT];
     float act_gain[NACT];
 };
+__device__ inline int cand_a(int v) { return v & 0xffff; }
+__device__ inline int cand_b(int v) { return v >> 16; }
 
 // ONX[x] bit b: body x is body b or one of its ancestors (x >= 1).  Indexed by the compile-time x of an
 // unrolled loop and shifted by the lane-varying b, so "is x on b's path" costs one shift and no memory load
@@ -76,13 +77,11 @@ template <typename T>
 constexpr ModelTab<T> make_tab() {
     ModelTab<T> m{};
     for (int b = 0; b < NB; b++) {
-        m.parent[b] = body_parent[b]; m.dof0[b] = body_dof0[b]; m.ndof[b] = body_ndof[b];
+        m.dof0[b] = body_dof0[b]; m.ndof[b] = body_ndof[b];
         m.mass[b] = (T)body_mass[b];
-        for (int i = 0; i < 3; i++) { m.toff[b][i] = (T)body_toff[3 * b + i]; m.com[b][i] = (T)body_com[3 * b + i]; }
-        for (int i = 0; i < 9; i++) { m.Roff[b][i] = (T)body_Roff[9 * b + i]; m.inertia[b][i] = (T)body_inertia[9 * b + i]; }
+        for (int i = 0; i < 3; i++) m.com[b][i] = (T)body_com[3 * b + i];
+        for (int i = 0; i < 9; i++) m.inertia[b][i] = (T)body_inertia[9 * b + i];
         m.nlink[b] = 0; m.link0[b] = -1;
-        for (int x = 0; x < NB; x++) m.onpath[b][x] = 0;
-        for (int x = b; x > 0; x = body_parent[x]) m.onpath[b][x] = 1;
     }
     for (int l = 0; l < NLINK; l++) {
         const int b = link_body[l];
@@ -93,19 +92,19 @@ constexpr ModelTab<T> make_tab() {
         for (int i = 0; i < 9; i++) m.linertia[l][i] = (T)link_inertia[9 * l + i];
     }
     for (int d = 0; d < NDOF; d++) {
-        m.daxis[d] = dof_axis[d]; m.dsign[d] = (T)dof_sign[d]; m.lo[d] = (T)dof_lo[d]; m.hi[d] = (T)dof_hi[d];
+        m.lo[d] = (T)dof_lo[d]; m.hi[d] = (T)dof_hi[d];
         m.damp[d] = (T)dof_damping[d];
     }
     int c = 0;
     for (int g = 0; g < NGEOM; g++) {
-        m.gbody[g] = geom_body[g]; m.gtype[g] = geom_type[g]; m.gr[g] = (T)geom_r[g];
+        m.gbody[g] = geom_body[g]; m.gr[g] = (T)geom_r[g];
         for (int i = 0; i < 3; i++) { m.gp1[g][i] = (T)geom_p1[3 * g + i]; m.gp2[g][i] = (T)geom_p2[3 * g + i]; }
         double h2 = 0;
         for (int i = 0; i < 3; i++) h2 += (geom_p2[3 * g + i] - geom_p1[3 * g + i]) * (geom_p2[3 * g + i] - geom_p1[3 * g + i]);
         m.gbr[g] = (T)(0.5 * csqrt(h2) + geom_r[g]);
-        for (int e = 0; e < (geom_type[g] == 0 ? 1 : 2); e++) { m.cand_a[c] = g; m.cand_b[c] = -1 - e; c++; }
+        for (int e = 0; e < (geom_type[g] == 0 ? 1 : 2); e++) { m.cand[c] = g | (int)((unsigned)(-1 - e) << 16); c++; }
     }
-    for (int k = 0; k < NPAIR; k++) { m.cand_a[c] = pair_a[k]; m.cand_b[c] = pair_b[k]; c++; }
+    for (int k = 0; k < NPAIR; k++) { m.cand[c] = pair_a[k] | (pair_b[k] << 16); c++; }
     for (int k = 0; k < NACT; k++) { m.act_dof[k] = hm::act_dof[k]; m.act_gain[k] = (float)hm::act_gain[k]; }
     return m;
 }
@@ -113,10 +112,10 @@ constexpr ModelTab<T> make_tab() {
 static __constant__ ModelTab<float> kTabF = make_tab<float>();   // per translation unit
 static __constant__ ModelTab<double> kTabD = make_tab<double>();
 template <typename T> __device__ inline const ModelTab<T>& tab();
-#ifdef HUM_TAB_LDS
+#ifdef HUM_TAB_LDS   // measured slower than __constant__ (24.3M vs 25.1M env-steps/s): opt-in experiment
 // fp32: the cooperative kernel indexes the tables by lane (body, dof, geom, candidate), which from
 // __constant__ memory are per-lane vector-memory loads with L1/L2 latency on every dependent chain.  Each
-// block keeps its own 4.5 KB LDS copy instead, filled once per launch by load_tab_lds.
+// block keeps its own 2.9 KB LDS copy instead, filled once per launch by load_tab_lds.
 static __shared__ ModelTab<float> sTabF;
 template <> __device__ inline const ModelTab<float>& tab<float>() { return sTabF; }
 #else
@@ -1099,7 +1098,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         int ba = 0;
         T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
         if (c < NCAND_GROUND) {
-            const int ga = M.cand_a[c], e = -1 - M.cand_b[c];
+            const int cv = M.cand[c], ga = cand_a(cv), e = -1 - cand_b(cv);
             const T* p = C.gp[ga][e];
             d = basez + p[2] - M.gr[ga];
             hit = d < (T)P.contact_thresh;
@@ -1118,7 +1117,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             const int k = r0 + l;
             bool maybe = false;
             if (k < NPAIR) {
-                const int ga = M.cand_a[NCAND_GROUND + k], gb = M.cand_b[NCAND_GROUND + k];
+                const int cv = M.cand[NCAND_GROUND + k], ga = cand_a(cv), gb = cand_b(cv);
                 T dm[3];
 #pragma unroll
                 for (int i = 0; i < 3; i++) dm[i] = (C.gp[ga][0][i] + C.gp[ga][1][i]) - (C.gp[gb][0][i] + C.gp[gb][1][i]);
@@ -1141,7 +1140,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #ifdef HUM_CHECK_LINKS
                 if ((unsigned)k >= (unsigned)NPAIR) atomicAdd(&g_check[4], 1u);
 #endif
-                const int ga = M.cand_a[NCAND_GROUND + k], gb = M.cand_b[NCAND_GROUND + k];
+                const int cv = M.cand[NCAND_GROUND + k], ga = cand_a(cv), gb = cand_b(cv);
                 T ca[3], cb[3], dv[3];
                 seg_seg(C.gp[ga][0], C.gp[ga][1], C.gp[gb][0], C.gp[gb][1], ca, cb);
 #pragma unroll
