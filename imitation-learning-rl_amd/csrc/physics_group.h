@@ -65,6 +65,29 @@ constexpr unsigned onx_mask(int x) {
 __device__ inline bool on_path(int x, int b) {   // b < 0: no body
     return b >= 0 && ((onx_mask(x) >> (b & 31)) & 1u);
 }
+// small per-body / per-geom integers packed into 64-bit constants (field width W bits, entry i at bit W*i):
+// a lane-indexed lookup is a shift and a mask instead of a vector-memory load
+template <int W, int N>
+constexpr unsigned long long pack_bits(const int (&v)[N], int off = 0) {
+    unsigned long long m = 0;
+    for (int i = 0; i < N - off && W * i < 64; i++) m |= (unsigned long long)v[off + i] << (W * i);
+    return m;
+}
+__device__ inline int body_ndof_l(int b) { return (int)((pack_bits<2>(body_ndof) >> (2 * b)) & 3u); }
+__device__ inline int body_dof0_l(int b) { return (int)((pack_bits<5>(body_dof0) >> (5 * b)) & 31u); }
+struct LinkInfo { int nlink[NB], link0[NB]; };
+constexpr LinkInfo link_info() {
+    LinkInfo r{};
+    for (int b = 0; b < NB; b++) { r.nlink[b] = 0; r.link0[b] = 0; }
+    for (int l = NLINK - 1; l >= 0; l--) { r.nlink[link_body[l]]++; r.link0[link_body[l]] = l; }
+    return r;
+}
+constexpr LinkInfo LINKS = link_info();
+__device__ inline int body_nlink_l(int b) { return (int)((pack_bits<2>(LINKS.nlink) >> (2 * b)) & 3u); }
+__device__ inline int body_link0_l(int b) { return (int)((pack_bits<4>(LINKS.link0) >> (4 * b)) & 15u); }
+__device__ inline int geom_body_l(int g) {   // g < 16 from one constant, g = 16 the other
+    return g < 16 ? (int)((pack_bits<4>(geom_body) >> (4 * (g & 15))) & 15u) : geom_body[16];
+}
 
 constexpr double csqrt(double x) {   // constexpr Newton square root (model constants only)
     if (x <= 0) return 0;
@@ -686,10 +709,20 @@ __device__ inline int lvl_sel(int g, int (*f)(int)) {   // per-group compile-tim
     const int v0 = f(LVL_BODY[LV][0]), v1 = f(LVL_BODY[LV][1]), v2 = f(LVL_BODY[LV][2]), v3 = f(LVL_BODY[LV][3]);
     return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
 }
+// joint damping of the group's body's j-th dof (0 past its dof count), selected among compile-time constants
+template <int LV, typename T>
+__device__ __attribute__((always_inline)) inline T lvl_damp(int g, int j) {
+    T v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int x = LVL_BODY[LV][i];
+        v[i] = j < body_ndof[x] ? (T)dof_damping[body_dof0[x] + j] : T(0);
+    }
+    return g == 0 ? v[0] : (g == 1 ? v[1] : (g == 2 ? v[2] : v[3]));
+}
 
 template <typename T, int LV>
 __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt) {
-    const ModelTab<T>& M = tab<T>();
     auto& A = S.x.aba;
     const int b = lvl_sel<LV>(g, [](int x) { return x; });
     const int k = lvl_sel<LV>(g, [](int x) { return body_ndof[x]; });
@@ -722,7 +755,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 #pragma unroll
         for (int e = 0; e < 6; e++) sp += Sc[j][e] * pAb[e];
         T t = S.tau[d] - sp;
-        if (P.joint_damping) t -= M.damp[d] * S.nu[6 + d];
+        if (P.joint_damping) t -= lvl_damp<LV, T>(g, j) * S.nu[6 + d];
         uj[j] = on ? t : T(0);
     }
 #pragma unroll
@@ -735,7 +768,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
             D[3 * i + j] = t;
         }
         const bool on = i < k;
-        if (P.joint_damping) D[4 * i] += on ? dt * M.damp[on ? d0 + i : d0] : T(0);
+        if (P.joint_damping) D[4 * i] += dt * lvl_damp<LV, T>(g, i);
         D[4 * i] = on ? D[4 * i] : T(1);   // identity pivot for padded dofs
     }
     small_inverse<T, 3>(D, Di);
@@ -903,7 +936,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             }
         }
         T cb[6] = {0, 0, 0, 0, 0, 0};
-        const int k = M.ndof[b], d0 = M.dof0[b];
+        const int k = body_ndof_l(b), d0 = body_dof0_l(b);
         for (int j = 0; j < k; j++) {
             const int d = d0 + j;
             T Sq[6], cr[6];
@@ -942,8 +975,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         pA[0] -= c3[1] * mg;
         pA[1] -= -c3[0] * mg;
         pA[5] -= mg;
-        for (int q = 0; q < M.nlink[b]; q++) {   // Bullet per-link velocity damping
-            const int lk = M.link0[b] + q;
+        for (int q = 0; q < body_nlink_l(b); q++) {   // Bullet per-link velocity damping
+            const int lk = body_link0_l(b) + q;
             T cl[3], vc[3], Iw[9], wI[3];
 #pragma unroll
             for (int i = 0; i < 3; i++) cl[i] = ob[i] + Rb[3 * i] * M.lcom[lk][0] + Rb[3 * i + 1] * M.lcom[lk][1] + Rb[3 * i + 2] * M.lcom[lk][2];
@@ -1040,7 +1073,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
     auto& C = S.x.cr;
     for (int g = l; g < NGEOM; g += GL) {
-        const int b = M.gbody[g];
+        const int b = geom_body_l(g);
 #pragma unroll
         for (int i = 0; i < 3; i++) {
             C.gp[g][0][i] = S.o[b][i] + S.R[b][3 * i] * M.gp1[g][0] + S.R[b][3 * i + 1] * M.gp1[g][1] + S.R[b][3 * i + 2] * M.gp1[g][2];
