@@ -52,6 +52,13 @@ struct ModelTab {
 __device__ inline int cand_a(int v) { return v & 0xffff; }
 __device__ inline int cand_b(int v) { return v >> 16; }
 
+constexpr double csqrt(double x) {   // constexpr Newton square root (model constants only)
+    if (x <= 0) return 0;
+    double r = x > 1 ? x : 1;
+    for (int i = 0; i < 100; i++) r = 0.5 * (r + x / r);
+    return r;
+}
+
 // ONX[x] bit b: body x is body b or one of its ancestors (x >= 1).  Indexed by the compile-time x of an
 // unrolled loop and shifted by the lane-varying b, so "is x on b's path" costs one shift and no memory load
 // (a lane-varying table lookup is a vector-memory load with its full latency on the dependency chain).
@@ -88,11 +95,85 @@ __device__ inline int body_link0_l(int b) { return (int)((pack_bits<4>(LINKS.lin
 __device__ inline int geom_body_l(int g) {   // g < 16 from one constant, g = 16 the other
     return g < 16 ? (int)((pack_bits<4>(geom_body) >> (4 * (g & 15))) & 15u) : geom_body[16];
 }
+// geom radius: a 3-bit code per geom (7 distinct radii) selects among exact compile-time constants
+struct RadiusCodes { int code[NGEOM]; double val[8]; int n; };
+constexpr RadiusCodes radius_codes() {
+    RadiusCodes r{};
+    r.n = 0;
+    for (int g = 0; g < NGEOM; g++) {
+        int c = -1;
+        for (int i = 0; i < r.n; i++) if (r.val[i] == geom_r[g]) c = i;
+        if (c < 0) { c = r.n; r.val[r.n++] = geom_r[g]; }
+        r.code[g] = c;
+    }
+    return r;
+}
+constexpr RadiusCodes RCODES = radius_codes();
+static_assert(RCODES.n <= 8, "3-bit radius codes");
+template <typename T>
+__device__ __attribute__((always_inline)) inline T geom_r_l(int g) {
+    const int c = (int)((pack_bits<3>(RCODES.code) >> (3 * g)) & 7u);
+    T r = (T)RCODES.val[0];
+#pragma unroll
+    for (int i = 1; i < RCODES.n; i++) r = c == i ? (T)RCODES.val[i] : r;
+    return r;
+}
 
-constexpr double csqrt(double x) {   // constexpr Newton square root (model constants only)
-    if (x <= 0) return 0;
-    double r = x > 1 ? x : 1;
-    for (int i = 0; i < 100; i++) r = 0.5 * (r + x / r);
+// contact candidates per (round, lane): 16-bit descriptors packed four lanes per 64-bit constant, so a
+// lane-indexed candidate costs a few selects and shifts and neither a table load (whose latency sat on the
+// chain of every round of every substep) nor registers held across the substep loop
+constexpr int CC_GROUND = (NCAND_GROUND + 15) / 16, CC_PAIR = (NPAIR + 15) / 16;
+struct CandDesc { unsigned long long g[CC_GROUND][4], p[CC_PAIR][4]; };
+constexpr CandDesc cand_desc() {
+    CandDesc d{};
+    int gl[NCAND_GROUND] = {}, el[NCAND_GROUND] = {}, c = 0;
+    for (int g = 0; g < NGEOM; g++)
+        for (int e = 0; e < (geom_type[g] == 0 ? 1 : 2); e++) { gl[c] = g; el[c] = e; c++; }
+    for (int r = 0; r < CC_GROUND; r++)
+        for (int l = 0; l < 16; l++) {
+            const int k = 16 * r + l;   // geom | endpoint << 5 | body << 6; 0xffff: none
+            const unsigned long long v = k < NCAND_GROUND ? (unsigned)(gl[k] | el[k] << 5 | geom_body[gl[k]] << 6) : 0xffffu;
+            d.g[r][l >> 2] |= v << (16 * (l & 3));
+        }
+    for (int r = 0; r < CC_PAIR; r++)
+        for (int l = 0; l < 16; l++) {
+            const int k = 16 * r + l;   // ga | gb << 5; 0xffff: none
+            const unsigned long long v = k < NPAIR ? (unsigned)(pair_a[k] | pair_b[k] << 5) : 0xffffu;
+            d.p[r][l >> 2] |= v << (16 * (l & 3));
+        }
+    return d;
+}
+constexpr CandDesc CDESC = cand_desc();
+__device__ __attribute__((always_inline)) inline int lane16(int l, unsigned long long c0, unsigned long long c1,
+                                                            unsigned long long c2, unsigned long long c3) {
+    const int q = l >> 2;
+    const unsigned long long c = q == 0 ? c0 : (q == 1 ? c1 : (q == 2 ? c2 : c3));
+    return (int)((c >> (16 * (l & 3))) & 0xffffu);
+}
+// bounding radius |p2 - p1| / 2 + r: a 4-bit code per geom (10 distinct values) over exact constants
+struct BrCodes { int code[NGEOM]; double val[16]; int n; };
+constexpr BrCodes br_codes() {
+    BrCodes r{};
+    r.n = 0;
+    for (int g = 0; g < NGEOM; g++) {
+        double h2 = 0;
+        for (int i = 0; i < 3; i++) h2 += (geom_p2[3 * g + i] - geom_p1[3 * g + i]) * (geom_p2[3 * g + i] - geom_p1[3 * g + i]);
+        const double v = 0.5 * csqrt(h2) + geom_r[g];
+        int c = -1;
+        for (int i = 0; i < r.n; i++) if (r.val[i] == v) c = i;
+        if (c < 0) { c = r.n; r.val[r.n++] = v; }
+        r.code[g] = c;
+    }
+    return r;
+}
+constexpr BrCodes BRCODES = br_codes();
+static_assert(BRCODES.n <= 16, "4-bit bounding-radius codes");
+template <typename T>
+__device__ __attribute__((always_inline)) inline T geom_br_l(int g) {
+    const int c = g < 16 ? (int)((pack_bits<4>(BRCODES.code) >> (4 * (g & 15))) & 15u) : BRCODES.code[16];
+    T r = (T)BRCODES.val[0];
+#pragma unroll
+    for (int i = 1; i < BRCODES.n; i++) r = c == i ? (T)BRCODES.val[i] : r;
     return r;
 }
 
@@ -1109,6 +1190,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     int nc = 0, over = 0;
     const T basez = S.st[2];
     const unsigned long long below16 = (lanemask_lt >> gbit) & 0xFFFFull;
+    // the candidate descriptors below are loop-invariant: an opaque copy of the lane index keeps the
+    // compiler from hoisting them out of the substep loop into registers held across every phase
+    int lc = l;
+    asm volatile("" : "+v"(lc));
     auto emit = [&](bool hit, int ba, int bb, const T* pa, const T* pb, const T* n, T d) {
         const unsigned long long bm = (__ballot(hit) >> gbit) & 0xFFFFull;
         const int pos = nc + __popcll(bm & below16);
@@ -1125,18 +1210,20 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         }
         nc += __popcll(bm);
     };
-    for (int r0 = 0; r0 < NCAND_GROUND; r0 += GL) {   // sphere / capsule end vs plane (cheap, exact)
-        const int c = r0 + l;
+#pragma unroll
+    for (int r = 0; r < CC_GROUND; r++) {   // sphere / capsule end vs plane (cheap, exact)
+        const int gd = lane16(lc, CDESC.g[r][0], CDESC.g[r][1], CDESC.g[r][2], CDESC.g[r][3]);
         bool hit = false;
         int ba = 0;
         T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
-        if (c < NCAND_GROUND) {
-            const int cv = M.cand[c], ga = cand_a(cv), e = -1 - cand_b(cv);
+        if (gd != 0xffff) {
+            const int ga = gd & 31, e = (gd >> 5) & 1;
+            const T gr = geom_r_l<T>(ga);
             const T* p = C.gp[ga][e];
-            d = basez + p[2] - M.gr[ga];
+            d = basez + p[2] - gr;
             hit = d < (T)P.contact_thresh;
-            ba = M.gbody[ga];
-            pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - M.gr[ga];
+            ba = gd >> 6;
+            pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - gr;
         }
         emit(hit, ba, -1, pa, pa, n, d);
     }
@@ -1146,19 +1233,20 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         int* surv = reinterpret_cast<int*>(&C.row[MAXR_LDS - 3][0]);
         const T reach = (T)P.contact_thresh + (T)1e-3;
         int ns = 0;
-        for (int r0 = 0; r0 < NPAIR; r0 += GL) {
-            const int k = r0 + l;
+#pragma unroll
+        for (int r = 0; r < CC_PAIR; r++) {
+            const int pd = lane16(lc, CDESC.p[r][0], CDESC.p[r][1], CDESC.p[r][2], CDESC.p[r][3]);
             bool maybe = false;
-            if (k < NPAIR) {
-                const int cv = M.cand[NCAND_GROUND + k], ga = cand_a(cv), gb = cand_b(cv);
+            if (pd != 0xffff) {
+                const int ga = pd & 31, gb = pd >> 5;
                 T dm[3];
 #pragma unroll
                 for (int i = 0; i < 3; i++) dm[i] = (C.gp[ga][0][i] + C.gp[ga][1][i]) - (C.gp[gb][0][i] + C.gp[gb][1][i]);
-                const T rr = M.gbr[ga] + M.gbr[gb] + reach;
+                const T rr = geom_br_l<T>(ga) + geom_br_l<T>(gb) + reach;
                 maybe = dot3(dm, dm) < T(4) * rr * rr;   // |ma - mb| < rr with ma = (p1 + p2) / 2
             }
             const unsigned long long bm = (__ballot(maybe) >> gbit) & 0xFFFFull;
-            if (maybe) surv[ns + __popcll(bm & below16)] = k;
+            if (maybe) surv[ns + __popcll(bm & below16)] = pd;   // survivors in pair order: ga | gb << 5
             ns += __popcll(bm);
         }
         wave_sync();
@@ -1169,17 +1257,16 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             int ba = 0, bb = -1;
             T pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
             if (j < ns) {
-                const int k = surv[j];
+                const int pd = surv[j], ga = pd & 31, gb = pd >> 5;
 #ifdef HUM_CHECK_LINKS
-                if ((unsigned)k >= (unsigned)NPAIR) atomicAdd(&g_check[4], 1u);
+                if ((unsigned)ga >= (unsigned)NGEOM || (unsigned)gb >= (unsigned)NGEOM) atomicAdd(&g_check[4], 1u);
 #endif
-                const int cv = M.cand[NCAND_GROUND + k], ga = cand_a(cv), gb = cand_b(cv);
                 T ca[3], cb[3], dv[3];
                 seg_seg(C.gp[ga][0], C.gp[ga][1], C.gp[gb][0], C.gp[gb][1], ca, cb);
 #pragma unroll
                 for (int i = 0; i < 3; i++) dv[i] = ca[i] - cb[i];
                 const T dist = sqrt(dot3(dv, dv));
-                const T ra = M.gr[ga], rb = M.gr[gb];
+                const T ra = geom_r_l<T>(ga), rb = geom_r_l<T>(gb);
                 d = dist - ra - rb;
                 hit = d < (T)P.contact_thresh && dist > (T)1e-9;
                 if (hit) {
@@ -1191,8 +1278,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                         pb[i] = cb[i] + rb * n[i];
                     }
                 }
-                ba = M.gbody[ga];
-                bb = M.gbody[gb];
+                ba = geom_body_l(ga);
+                bb = geom_body_l(gb);
             }
             emit(hit, ba, bb, pa, pb, n, d);
         }
