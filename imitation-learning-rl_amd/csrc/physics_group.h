@@ -805,6 +805,8 @@ __device__ __attribute__((always_inline)) inline T lvl_damp(int g, int j) {
 template <typename T, int LV>
 __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt) {
     auto& A = S.x.aba;
+    // the level's largest dof count (1, 3, 1, 2): smaller bodies of the level are padded to it
+    constexpr int KM = [] { int m = 0; for (int i = 0; i < 4; i++) m = body_ndof[LVL_BODY[LV][i]] > m ? body_ndof[LVL_BODY[LV][i]] : m; return m; }();
     const int b = lvl_sel<LV>(g, [](int x) { return x; });
     const int k = lvl_sel<LV>(g, [](int x) { return body_ndof[x]; });
     const int d0 = lvl_sel<LV>(g, [](int x) { return body_dof0[x]; });
@@ -825,7 +827,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
     if constexpr (LVL_KID[LV][0][1] >= 0)
         add_kid(g == 0 ? LVL_KID[LV][0][1] : (g == 1 ? LVL_KID[LV][1][1] : (g == 2 ? LVL_KID[LV][2][1] : LVL_KID[LV][3][1])));
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
+    for (int j = 0; j < KM; j++) {
         const bool on = j < k;
         const int d = on ? d0 + j : d0;
         load_sc(S, d, Sc[j]);
@@ -840,9 +842,9 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
         uj[j] = on ? t : T(0);
     }
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < KM; i++) {
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
+        for (int j = 0; j < KM; j++) {
             T t = 0;
 #pragma unroll
             for (int e = 0; e < 6; e++) t += Sc[i][e] * U[j][e];
@@ -852,14 +854,16 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
         if (P.joint_damping) D[4 * i] += dt * lvl_damp<LV, T>(g, i);
         D[4 * i] = on ? D[4 * i] : T(1);   // identity pivot for padded dofs
     }
-    small_inverse<T, 3>(D, Di);
 #pragma unroll
-    for (int j = 0; j < 3; j++)
+    for (int q = 0; q < 9; q++) Di[q] = q % 4 == 0 ? T(1) : T(0);   // identity outside the KM block
+    small_inverse<T, KM>(D, Di);
+#pragma unroll
+    for (int j = 0; j < KM; j++)
 #pragma unroll
         for (int e = 0; e < 6; e++) {
             T t = 0;
 #pragma unroll
-            for (int i = 0; i < 3; i++) t += U[i][e] * Di[3 * i + j];
+            for (int i = 0; i < KM; i++) t += U[i][e] * Di[3 * i + j];
             W[j][e] = t;
         }
     // Ia = IA - W U^T (in place), pa = pA + Ia c + W u
@@ -869,7 +873,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
         for (int cc = r; cc < 6; cc++) {
             T t = IA[sidx(r, cc)];
 #pragma unroll
-            for (int j = 0; j < 3; j++) t -= W[j][r] * U[j][cc];
+            for (int j = 0; j < KM; j++) t -= W[j][r] * U[j][cc];
             IA[sidx(r, cc)] = t;
         }
     T pa[6];
@@ -878,7 +882,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
     for (int e = 0; e < 6; e++) {
         T t = pAb[e] + pa[e];
 #pragma unroll
-        for (int j = 0; j < 3; j++) t += W[j][e] * uj[j];
+        for (int j = 0; j < KM; j++) t += W[j][e] * uj[j];
         pa[e] = t;
     }
     // contribution to the parent in the body's own (now dead) slots; factorisation for passes 3 / responses.
@@ -888,7 +892,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 #pragma unroll
     for (int e = 0; e < 6; e++) A.pA[b][e] = pa[e];
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
+    for (int j = 0; j < KM; j++) {
         if (j < k) {
 #pragma unroll
             for (int e = 0; e < 6; e++) S.U[d0 + j][e] = U[j][e];
@@ -915,12 +919,13 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
     const int p = sel([](int x) { return body_parent[x]; });
     const int k = sel([](int x) { return body_ndof[x]; });
     const int d0 = sel([](int x) { return body_dof0[x]; });
+    constexpr int KM = [] { int m = 0; for (int i = 0; i < 4; i++) m = body_ndof[FWD_BODY[LV][i]] > m ? body_ndof[FWD_BODY[LV][i]] : m; return m; }();
     const T vmax = (T)P.max_coord_vel;
     T ap[6], r[3], ab[6];
 #pragma unroll
     for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + A.c[b][e]; ab[e] = ap[e]; }
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
+    for (int j = 0; j < KM; j++) {
         const int d = j < k ? d0 + j : d0;
         T t = A.uu[d];
 #pragma unroll
@@ -928,10 +933,10 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
         r[j] = j < k ? t : T(0);
     }
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < KM; i++) {
         T t = 0;
 #pragma unroll
-        for (int j = 0; j < 3; j++) t += S.Dinv[b][3 * i + j] * r[j];   // padded block: identity, r = 0
+        for (int j = 0; j < KM; j++) t += S.Dinv[b][3 * i + j] * r[j];   // padded block: identity, r = 0
         const int d = i < k ? d0 + i : d0;
         T Sc[6];
         load_sc(S, d, Sc);
