@@ -119,9 +119,10 @@ struct PostPhys {   // physics-derived quantities calc_state reads (pybullet get
 // WalkerBase.calc_state (pybullet_envs/robot_locomotors.py) -> 42 float32 + side effects
 template <typename T>
 __device__ inline void calc_state(const T* st, const double* wt, float* obs42, float* joint_speeds, int& joints_at_limit,
-                                  PostPhys<T>& pp) {
+                                  PostPhys<T>& pp, const T* scs = nullptr) {
     Kin<T> K;
-    forward_kinematics(st + 3, st + 13, K);
+    if (scs) forward_kinematics_pre(st + 3, scs, K);   // hinge sin / cos of this state precomputed across lanes
+    else forward_kinematics(st + 3, st + 13, K);
     T parts[NPART][3];
     part_positions(K, parts);
     const double bpx = (double)st[0], bpy = (double)st[1];

@@ -187,14 +187,14 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
 
 // Post-physics part of step (low_level_env.py:481-526) + optional auto-reset; stores state, book, outputs.
 template <typename T>
-__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef) {
+__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef, const T* scs = nullptr) {
     const ClipDev& c = a.clips[b.clip];
     float obs[HUM_NOBS];
     // calc_state (:481) and robot_pos (:483-486)
     float js[NDOF];
     int jal;
     PostPhys<T> pp;
-    calc_state(st, b.wt, obs, js, jal, pp);
+    calc_state(st, b.wt, obs, js, jal, pp, scs);
     b.robot_pos[0] = pp.bx; b.robot_pos[1] = pp.by; b.robot_pos[2] = 0;
     // updateReward (:441-465)
     double dJ = 0, dV = 0;
@@ -374,7 +374,7 @@ __device__ inline float hier_update_reward_high(Book& b) {
 // step(action_dict) (hier_env.py:355-366) -> high_level_step (:538-571) or low_level_step (:583-641), after the
 // physics of a low step; stores state/book and writes the dict-shaped outputs.
 template <typename T>
-__device__ void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsigned& ef) {
+__device__ void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsigned& ef, const T* scs = nullptr) {
     const ClipDev& c = a.clips[b.clip];
     b.robot_pos[0] = b.bxy[0]; b.robot_pos[1] = b.bxy[1]; b.robot_pos[2] = 0;   // step(): :358-361
     float obs[HUM_NOBS], js[NDOF], o44[HUM_NOBS_HIGH];
@@ -406,7 +406,7 @@ __device__ void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsi
         agents = HUM_AGENT_LOW;
     } else {
         b.level_rem -= 1;                                                                   // :584
-        calc_state(st, b.wt, obs, js, jal, pp);                                             // :591
+        calc_state(st, b.wt, obs, js, jal, pp, scs);                                        // :591
         const float* act = a.act + (long)i * HUM_NACT;
         // updateReward (:494-522)
         double dJ = 0, dV = 0;
@@ -611,6 +611,16 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
             group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_rows_per_block(EPB_, a.P.lds_rows) * RW,
                                    l, ef);
     }
+    // hinge sin / cos of the final physics state, one dof per lane, for calc_state's kinematics on lane 0
+    T* scs = &sh[ge].x.aba.IA[0][0];
+    for (int d = l; d < NDOF; d += GL) {
+        T sn, cs;
+        if constexpr (sizeof(T) == 4) sincosf(S.st[13 + d], &sn, &cs);
+        else sincos(S.st[13 + d], &sn, &cs);
+        scs[2 * d] = sn;
+        scs[2 * d + 1] = cs;
+    }
+    wave_sync();
     PHASE_INIT;
     if (valid && l == 0) {
         Book b;
@@ -628,12 +638,12 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
                 for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
             }
             if (a.hier) {
-                hier_post(a, i, st, b, high, ef);
+                hier_post(a, i, st, b, high, ef, high ? nullptr : scs);   // high: the HBM state, not S.st
             } else {
                 float act[HUM_NACT];
 #pragma unroll
                 for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[(long)i * HUM_NACT + k];
-                post_step(a, i, st, b, act, ef);
+                post_step(a, i, st, b, act, ef, scs);
             }
         }
     }
