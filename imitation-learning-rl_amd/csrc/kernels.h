@@ -120,7 +120,7 @@ __device__ inline int draw(const KArgs& a, int i, Book& b, int lo, int hi) {
 // LowLevelHumanoidEnv.reset() / resetFromFrame() (low_level_env.py:224-305)
 template <typename T>
 __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* obs,
-                           unsigned& ef) {
+                           unsigned& ef, const T* scs = nullptr) {   // scs: the reset pose's hinge sin / cos
     const ClipDev& c = a.clips[b.clip];
     if (start_frame < 0) start_frame = draw(a, i, b, 0, c.max_frame - 5);   // :228
     // flat_env.reset(): restoreState -> zero velocities (all 17 joints overwritten below)
@@ -160,7 +160,8 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
     const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
     {
         Kin<T> K;
-        forward_kinematics(st + 3, st + 13, K);
+        if (scs) forward_kinematics_pre(st + 3, scs, K);
+        else forward_kinematics(st + 3, st + 13, K);
         T pp[NPART][3];
         part_positions(K, pp);
         const double rfx = (double)st[0] + (double)pp[PART_RIGHT_FOOT][0];
@@ -181,13 +182,14 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
     float js[NDOF];
     int jal;
     PostPhys<T> pp;
-    calc_state(st, b.wt, obs, js, jal, pp);                                 // :304-305
+    calc_state(st, b.wt, obs, js, jal, pp, scs);                            // :304-305
     ref_obs(c, b.frame, obs + 42, ef);
 }
 
 // Post-physics part of step (low_level_env.py:481-526) + optional auto-reset; stores state, book, outputs.
 template <typename T>
-__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef, const T* scs = nullptr) {
+__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef, const T* scs = nullptr,
+                          bool* defer_reset = nullptr) {   // defer_reset: the caller runs the auto-reset and the store
     const ClipDev& c = a.clips[b.clip];
     float obs[HUM_NOBS];
     // calc_state (:481) and robot_pos (:483-486)
@@ -263,6 +265,10 @@ __device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* ac
     a.rew[i] = (float)total;
     a.done[i] = done ? 1 : 0;
     if (a.frame_out) a.frame_out[i] = b.frame;
+    if (defer_reset) {
+        *defer_reset = done && (a.flags & HUM_STEP_AUTORESET);
+        return;
+    }
     if (done && (a.flags & HUM_STEP_AUTORESET)) {
         float o2[HUM_NOBS];
         reset_lane(a, i, st, b, -1, 0.0, o2, ef);
@@ -615,21 +621,21 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     T* scs = &sh[ge].x.aba.IA[0][0];
     for (int d = l; d < NDOF; d += GL) {
         T sn, cs;
-        if constexpr (sizeof(T) == 4) sincosf(S.st[13 + d], &sn, &cs);
-        else sincos(S.st[13 + d], &sn, &cs);
+        hinge_sincos(S.st[13 + d], &sn, &cs);
         scs[2 * d] = sn;
         scs[2 * d + 1] = cs;
     }
     wave_sync();
     PHASE_INIT;
+    Book b;
+    T st[HUM_NSTATE];
+    bool rst = false;
     if (valid && l == 0) {
-        Book b;
         load_book(a, i, b);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
             nonfinite_outputs(a, i, b.frame);
         } else {
-            T st[HUM_NSTATE];
             if (high) {   // physics (if the wave ran it) is discarded: the HBM state is the current one
 #pragma unroll
                 for (int e = 0; e < HUM_NSTATE; e++) st[e] = ((const T*)a.phys)[(long)e * a.n + i];
@@ -643,8 +649,49 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
                 float act[HUM_NACT];
 #pragma unroll
                 for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[(long)i * HUM_NACT + k];
-                post_step(a, i, st, b, act, ef, scs);
+                post_step(a, i, st, b, act, ef, scs, &rst);
             }
+        }
+    }
+    if (!a.hier) {
+        // auto-reset (low-level env): lane 0 draws the start frame (reset_lane's first draw), the env's lanes
+        // compute the reset pose's hinge sin / cos, lane 0 finishes reset_lane with them and stores the lane
+        int* xch = reinterpret_cast<int*>(scs + 2 * NDOF);
+        if (valid && l == 0) {
+            int sf = -1;
+            if (rst) sf = draw(a, i, b, 0, a.clips[b.clip].max_frame - 5);   // low_level_env.py:228
+            xch[0] = sf;
+            xch[1] = b.clip;
+        }
+        wave_sync();
+        const int sf = valid ? xch[0] : -1;
+        T* scs_r = scs + 2 * NDOF + 2;
+        if (__ballot(sf >= 0) != 0) {
+            if (sf >= 0) {
+                const ClipDev& c = a.clips[xch[1]];
+                for (int d = l; d < NDOF; d += GL) {
+                    T q = T(0);
+#pragma unroll
+                    for (int j = 0; j < NREF; j++)
+                        if (JM_DOF[j] == d) q = (T)c.pos[sf * 14 + JM_COL[j]];
+                    T sn, cs;
+                    hinge_sincos(q, &sn, &cs);
+                    scs_r[2 * d] = sn;
+                    scs_r[2 * d + 1] = cs;
+                }
+            }
+            wave_sync();
+        }
+        if (valid && l == 0 && env_ok) {
+            if (rst) {
+                float o2[HUM_NOBS];
+                reset_lane(a, i, st, b, sf, 0.0, o2, ef, scs_r);
+                if (a.obs_reset) {
+#pragma unroll
+                    for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[(long)i * HUM_NOBS + k] = o2[k];
+                }
+            }
+            store_lane(a, i, st, b);
         }
     }
     PHASE(10);

@@ -98,6 +98,7 @@ __device__ inline void crf(const T* v, const T* f, T* r) {
 // post-multiply a 3x3 (row major) by an elementary rotation about axis `ax` with (c, s)
 template <typename T>
 __device__ inline void rot_post(T* M, int ax, T c, T s) {
+#pragma clang fp contract(on)   // per-expression fusion only: the same frames in every inlining context
     const int i = (ax + 1) % 3, j = (ax + 2) % 3;  // columns mixed by a rotation about `ax`
 #pragma unroll
     for (int r = 0; r < 3; r++) {
@@ -109,6 +110,7 @@ __device__ inline void rot_post(T* M, int ax, T c, T s) {
 
 template <typename T>
 __device__ inline void quat_to_mat(const T* q, T* R) {
+#pragma clang fp contract(on)   // per-expression fusion only: the same frames in every inlining context
     T x = q[0], y = q[1], z = q[2], w = q[3];
     R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
     R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
@@ -127,41 +129,12 @@ struct Kin {
 };
 
 template <typename T>
-__device__ inline void forward_kinematics(const T* quat, const T* q, Kin<T>& K) {
-    quat_to_mat(quat, K.R[0]);
-    K.o[0][0] = K.o[0][1] = K.o[0][2] = 0;
-#pragma unroll
-    for (int b = 1; b < NB; b++) {
-        const int p = body_parent[b];
-        T M[9];
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-            for (int c = 0; c < 3; c++)
-                M[3 * r + c] = K.R[p][3 * r] * (T)body_Roff[9 * b + c] + K.R[p][3 * r + 1] * (T)body_Roff[9 * b + 3 + c] +
-                               K.R[p][3 * r + 2] * (T)body_Roff[9 * b + 6 + c];
-#pragma unroll
-        for (int i = 0; i < 3; i++)
-            K.o[b][i] = K.o[p][i] + K.R[p][3 * i] * (T)body_toff[3 * b] + K.R[p][3 * i + 1] * (T)body_toff[3 * b + 1] +
-                        K.R[p][3 * i + 2] * (T)body_toff[3 * b + 2];
-#pragma unroll
-        for (int k = 0; k < body_ndof[b]; k++) {
-            const int d = body_dof0[b] + k, ax = dof_axis[d];
-            const T sg = (T)dof_sign[d];
-            K.u[d][0] = M[ax] * sg; K.u[d][1] = M[3 + ax] * sg; K.u[d][2] = M[6 + ax] * sg;
-            T sn, cs;
-            if constexpr (sizeof(T) == 4) sincosf(q[d], &sn, &cs);
-            else sincos(q[d], &sn, &cs);
-            rot_post(M, ax, cs, sg * sn);
-        }
-#pragma unroll
-        for (int i = 0; i < 9; i++) K.R[b][i] = M[i];
-    }
-}
+__device__ inline void forward_kinematics(const T* quat, const T* q, Kin<T>& K);   // below: via the _pre form
 
 // the same with the hinge angles' sin / cos precomputed (scs[2d] = sin q_d, scs[2d+1] = cos q_d)
 template <typename T>
 __device__ inline void forward_kinematics_pre(const T* quat, const T* scs, Kin<T>& K) {
+#pragma clang fp contract(on)   // per-expression fusion only: the same frames in every inlining context
     quat_to_mat(quat, K.R[0]);
     K.o[0][0] = K.o[0][1] = K.o[0][2] = 0;
 #pragma unroll
@@ -188,6 +161,21 @@ __device__ inline void forward_kinematics_pre(const T* quat, const T* scs, Kin<T
 #pragma unroll
         for (int i = 0; i < 9; i++) K.R[b][i] = M[i];
     }
+}
+
+// every kinematics evaluation goes through forward_kinematics_pre, so a state's frames are bit-identical
+// whether its hinge sin / cos were computed here or across lanes (cooperative kernel)
+template <typename T>
+__device__ inline void hinge_sincos(T q, T* sn, T* cs) {
+    if constexpr (sizeof(T) == 4) sincosf(q, sn, cs);
+    else sincos(q, sn, cs);
+}
+template <typename T>
+__device__ inline void forward_kinematics(const T* quat, const T* q, Kin<T>& K) {
+    T scs[2 * NDOF];
+#pragma unroll
+    for (int d = 0; d < NDOF; d++) hinge_sincos(q[d], &scs[2 * d], &scs[2 * d + 1]);
+    forward_kinematics_pre(quat, scs, K);
 }
 
 // motion subspace column of dof d (body b) at the common origin: [u; o_b x u]
@@ -891,6 +879,7 @@ __device__ inline int substep(const PhysParams& P, T* st, const T* tau, const La
 // world positions (relative to base COM) of the 33 parts; floor handled by the caller
 template <typename T>
 __device__ inline void part_positions(const Kin<T>& K, T (*pp)[3]) {
+#pragma clang fp contract(on)   // per-expression fusion only: the same frames in every inlining context
 #pragma unroll
     for (int k = 0; k < NPART; k++) {
         const int b = part_body[k];

@@ -965,8 +965,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         T* scs = &S.x.aba.IA[0][0];
         for (int d = l; d < NDOF; d += GL) {
             T sn, cs;
-            if constexpr (sizeof(T) == 4) sincosf(S.st[13 + d], &sn, &cs);
-            else sincos(S.st[13 + d], &sn, &cs);
+            hinge_sincos(S.st[13 + d], &sn, &cs);
             scs[2 * d] = sn;
             scs[2 * d + 1] = cs;
         }

@@ -340,3 +340,41 @@ def test_rollout_deterministic():
         env.close()
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_in_kernel_autoreset_equals_explicit_reset(precision):
+    """The step kernel's auto-reset (start frame drawn by lane 0, the reset pose's hinge sin / cos computed
+    across the env's lanes) leaves exactly the state, bookkeeping and reset obs that step-without-reset
+    followed by hum_reset (reset_kernel, one thread per lane) produces from the same RNG counters."""
+    import torch
+    n = 256
+    a_env = HumanoidVecEnv(n, clips=("motion02_04",), seed=11, precision=precision)
+    b_env = HumanoidVecEnv(n, clips=("motion02_04",), seed=11, precision=precision)
+    a_env.reset()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    checked = 0
+    for s in range(60):
+        act = (torch.rand(n, 17, device="cuda", generator=g) * 2 - 1).contiguous()
+        phys, book = a_env.get_state()
+        b_env.set_state(phys, book)
+        _, _, done_a, _ = a_env.step(act, autoreset=True)
+        done_a = done_a.cpu().numpy().astype(bool)
+        obs_reset_a = a_env.obs_reset.cpu().numpy().copy()
+        pa, ba = a_env.get_state()
+        _, _, done_b, _ = b_env.step(act, autoreset=False)
+        np.testing.assert_array_equal(done_b.cpu().numpy().astype(bool), done_a)
+        if done_a.any():
+            obs_b = b_env.reset(mask=done_a.astype(np.uint8)).cpu().numpy()
+            np.testing.assert_array_equal(obs_reset_a[done_a], obs_b[done_a])
+            checked += int(done_a.sum())
+        pb, bb = b_env.get_state()
+        np.testing.assert_array_equal(pa, pb)
+        bad = np.nonzero((ba != bb).any(axis=0))[0]
+        names = {v: k for k, v in N.BK.items()}
+        assert len(bad) == 0, "book columns differ: %s (lanes %s, max %.3g)" % (
+            [names.get(int(c), int(c)) for c in bad], np.nonzero((ba != bb).any(axis=1))[0][:8], np.abs(ba - bb).max())
+    a_env.close()
+    b_env.close()
+    assert checked > 0, "no lane finished an episode"
