@@ -583,7 +583,12 @@ template <typename T, int EPB_>
 __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     __shared__ GroupLDS<T> sh[EPB_];
     const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
-    const int i = blockIdx.x * EPB_ + ge;
+    // XCD-aware env mapping: the dispatcher deals blocks round-robin over the 8 XCDs (block b -> XCD b % 8),
+    // so consecutive blocks would put the 4-env (16/32-byte) slices of one SoA cache line into 8 different L2s,
+    // each fetching the whole line.  Give XCD x one contiguous run of blocks instead (a bijection for any grid).
+    const int nb = gridDim.x, xq = nb >> 3, xr = nb & 7, xcd = blockIdx.x & 7;
+    const int blk = xcd * xq + min(xcd, xr) + (blockIdx.x >> 3);
+    const int i = blk * EPB_ + ge;
     const bool valid = i < a.n;
     GroupLDS<T>& S = sh[ge];
 #ifdef HUM_WLOG_ON
