@@ -132,7 +132,7 @@ void hum_default_config(hum_config* c) {
     c->ang_damp = 0.04;
     c->limit_max_impulse = 100.0;
     c->max_coord_vel = 100.0;
-    c->max_contacts = 16;
+    c->max_contacts = HUM_MAX_CONTACTS;   // every candidate: no truncation
     c->self_collision = 1;
     c->joint_damping = 1;
     c->kernel = 1;
@@ -153,8 +153,9 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (cfg->envs_per_block != 1 && cfg->envs_per_block != 2 && cfg->envs_per_block != 4)
         return fail(HUM_ERR_ARG, "hum_create: envs_per_block must be 1, 2 or 4");
     if (cfg->lds_rows < 0) return fail(HUM_ERR_ARG, "hum_create: lds_rows must be >= 0");
-    if (cfg->max_contacts < 0 || cfg->max_contacts > (cfg->kernel == 1 ? MAXC_G : MAXC))
-        return fail(HUM_ERR_ARG, "hum_create: max_contacts out of range for the selected kernel");
+    static_assert(MAXC_G == HUM_MAX_CONTACTS && MAXC == HUM_MAX_CONTACTS, "contact list holds every candidate");
+    if (cfg->max_contacts < 0 || cfg->max_contacts > HUM_MAX_CONTACTS)
+        return fail(HUM_ERR_ARG, "hum_create: max_contacts out of range [0, HUM_MAX_CONTACTS]");
     HIPCHK(hipSetDevice(cfg->device));
     hum_env* e = new hum_env();
     e->cfg = *cfg;
@@ -168,7 +169,7 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (st == hipSuccess) {   // per-lane rows (kernel 0) or the per-block row spill regions (kernel 1)
         const int epb = cfg->envs_per_block;
         const size_t blocks = (n + epb - 1) / epb;
-        st = hipMalloc(&e->d.scratch, (cfg->kernel == 1 ? (size_t)grow_rows_per_block(epb, lds_rows_of(*cfg)) * RW * blocks
+        st = hipMalloc(&e->d.scratch, (cfg->kernel == 1 ? (size_t)grow_block_size(epb, lds_rows_of(*cfg)) * blocks
                                                           : (size_t)SCRATCH_PER_LANE * n) * e->real_size);
     }
     if (st == hipSuccess) st = hipMalloc((void**)&e->eflags, sizeof(unsigned));

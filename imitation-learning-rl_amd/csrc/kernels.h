@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++)
-            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_rows_per_block(EPB_, a.P.lds_rows) * RW,
+            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_block_size(EPB_, a.P.lds_rows),
                                    l, ef);
     }
     // hinge sin / cos of the final physics state, one dof per lane, for calc_state's kinematics on lane 0
@@ -755,7 +755,8 @@ __global__ void __launch_bounds__(256) reset_kernel(KArgs a) {
 static __global__ void init_kernel(KArgs a) {   // fresh lanes: clip 0, no mode, RNG key from (seed, global lane)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
-    const unsigned long long k = splitmix64(a.seed + (unsigned long long)(a.lane_offset + i));
+    // non-additive key (oracle/oracle.py::lane_key): (seed s, lane i+1) and (seed s+1, lane i) differ
+    const unsigned long long k = splitmix64(splitmix64(a.seed) ^ (unsigned long long)(a.lane_offset + i));
     a.bi[6 * a.n + i] = (int)(unsigned)(k & 0xffffffffull);
     a.bi[7 * a.n + i] = (int)(unsigned)(k >> 32);
 }

@@ -19,8 +19,14 @@
 namespace hk {
 
 constexpr int GL = 16;                       // lanes per env
-constexpr int MAXC_G = 16;                   // contact cap of the cooperative kernel
-constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // 65 rows
+// contacts: the first MAXC_LDS of an env's contact list live in LDS, the rest (rare: a lying humanoid with
+// many self contacts) in the env's slice of its block's global spill region; the list holds every candidate
+// (MAXC_G = 29 ground points + 66 geom pairs), so nothing is ever dropped
+constexpr int MAXC_LDS = 16;
+constexpr int MAXC_G = MAXC;                 // = NCAND_ALL (physics.h)
+constexpr int CW = 12;                       // contact entry: ba, bb, pa[3], pb[3], n[3], d
+constexpr int MAXL_G = 2 * NDOF;             // limit rows (one per violated side)
+constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // rows of one env: limits + (normal + 2 frictions) per contact
 // constraint row layout (T units): J and M^-1 J^T interleaved per dof ([2q] = J_q, [2q+1] = (M^-1 J^T)_q), a
 // zero pair (read by the lanes without a second velocity component), then two 16-byte scalar quads:
 // b, hi, lambda, 1/(J M^-1 J^T) and mu, c = J . (M^-1 J^T of the predecessor row), next3, next3_ln (ints).
@@ -260,9 +266,9 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
         } aba;
         struct {   // contacts + constraint rows
             T gp[NGEOM][2][3];
-            T con[MAXC_G][12];
+            T con[MAXC_LDS][CW];
             alignas(16) T row[MAXR_LDS][RW];
-            int rdesc[MAXR_G];   // limit rows: dof | side << 8
+            int rdesc[MAXL_G];   // limit rows: dof | side << 8
         } cr;
     } x;
 };
@@ -285,6 +291,13 @@ __device__ __attribute__((always_inline)) inline int pool_off(int p) {   // byte
     return s * (int)sizeof(GroupLDS<T>) + (int)offsetof(GroupLDS<T>, x.cr.row) + i * RW * (int)sizeof(T);
 }
 __host__ __device__ constexpr int grow_rows_per_block(int epb, int cap) { return epb * MAXR_G - cap; }
+// a block's global spill region (T units): rows past the LDS pool, then each env's contacts past MAXC_LDS
+__host__ __device__ constexpr long grow_block_size(int epb, int cap) {
+    return (long)grow_rows_per_block(epb, cap) * RW + (long)epb * (MAXC_G - MAXC_LDS) * CW;
+}
+__host__ __device__ constexpr long gcon_offset(int epb, int cap, int ge) {
+    return (long)grow_rows_per_block(epb, cap) * RW + (long)ge * (MAXC_G - MAXC_LDS) * CW;
+}
 
 // ---- diagnostics (never in the shipped library): -DHUM_PHASE_TIMING = per-phase s_memtime counters (global
 // atomics: they slow the kernel and skew it between XCDs) + the per-block work log; -DHUM_WAVE_LOG = the work
@@ -691,7 +704,15 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         } else {
             const int cidx = r < enl + enc ? r - enl : (r - enl - enc) >> 1;
             const int f = r < enl + enc ? 0 : 1 + ((r - enl - enc) & 1);
-            const T* ce = C.con[cidx];
+            T ce[CW];
+            if (cidx < MAXC_LDS) {
+#pragma unroll
+                for (int k = 0; k < CW; k++) ce[k] = C.con[cidx][k];
+            } else {   // spilled contact (nontemporal: keeps the LDS path's loads ds_read, not flat)
+                const T* gc = gblock + gcon_offset(EPB_, cap, e) + (long)(cidx - MAXC_LDS) * CW;
+#pragma unroll
+                for (int k = 0; k < CW; k++) ce[k] = __builtin_nontemporal_load(gc + k);
+            }
             ba = (int)ce[0];
             bb = (int)ce[1];
             const T pa[3] = {ce[2], ce[3], ce[4]}, pb[3] = {ce[5], ce[6], ce[7]}, n[3] = {ce[8], ce[9], ce[10]};
@@ -1198,16 +1219,30 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     // compiler from hoisting them out of the substep loop into registers held across every phase
     int lc = l;
     asm volatile("" : "+v"(lc));
+    T* gcon = gblock + gcon_offset(EPB_, P.lds_rows, ge);   // this env's contacts past MAXC_LDS
     auto emit = [&](bool hit, int ba, int bb, const T* pa, const T* pb, const T* n, T d) {
         const unsigned long long bm = (__ballot(hit) >> gbit) & 0xFFFFull;
         const int pos = nc + __popcll(bm & below16);
         if (hit) {
             if (pos < maxc) {
-                T* e = C.con[pos];
-                e[0] = (T)ba; e[1] = (T)bb;
+                if (pos < MAXC_LDS) {
+                    T* e = C.con[pos];
+                    e[0] = (T)ba; e[1] = (T)bb;
 #pragma unroll
-                for (int i = 0; i < 3; i++) { e[2 + i] = pa[i]; e[5 + i] = pb[i]; e[8 + i] = n[i]; }
-                e[11] = d;
+                    for (int i = 0; i < 3; i++) { e[2 + i] = pa[i]; e[5 + i] = pb[i]; e[8 + i] = n[i]; }
+                    e[11] = d;
+                } else {
+                    T* e = gcon + (long)(pos - MAXC_LDS) * CW;
+                    __builtin_nontemporal_store((T)ba, e);
+                    __builtin_nontemporal_store((T)bb, e + 1);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) {
+                        __builtin_nontemporal_store(pa[i], e + 2 + i);
+                        __builtin_nontemporal_store(pb[i], e + 5 + i);
+                        __builtin_nontemporal_store(n[i], e + 8 + i);
+                    }
+                    __builtin_nontemporal_store(d, e + 11);
+                }
             } else {
                 over = 1;
             }

@@ -43,6 +43,7 @@ extern "C" {
 #define HUM_NACT_HIGH 2    /* high_level_act_space shape (cos, sin of the heading), hier_env.py:53-55 */
 #define HUM_NAUX 12     /* RewardLogCallback terms per lane, layout HUM_AUX_* below */
 #define HUM_MAX_CLIPS 8
+#define HUM_MAX_CONTACTS 95  /* every contact candidate: 29 sphere / capsule-end ground points + 66 geom pairs */
 
 /* status codes */
 #define HUM_OK 0
@@ -62,7 +63,7 @@ extern "C" {
 /* error flag bits (hum_get_error_flags) */
 #define HUM_EFLAG_NONFINITE_ACTION 1u   /* humanoid.py:55 assert np.isfinite(a).all(): lane not stepped */
 #define HUM_EFLAG_VEL_ROW 2u            /* frame beyond the velocity table (motion13_13): clamped row used */
-#define HUM_EFLAG_CONTACT_OVERFLOW 4u   /* more contact candidates than max_contacts */
+#define HUM_EFLAG_CONTACT_OVERFLOW 4u   /* more contacts than a lowered max_contacts (never with the default) */
 
 /* bookkeeping layout (doubles; integers stored exactly) */
 enum {
@@ -72,7 +73,7 @@ enum {
     HUM_BK_DELTA_JOINTS = 20, HUM_BK_DELTA_VEL_JOINTS = 21, HUM_BK_BODY_POSTURE = 22, HUM_BK_ELECTRICITY = 23,
     HUM_BK_JOINT_LIMIT = 24, HUM_BK_ALIVE = 25, HUM_BK_DELTA_LOW_TARGET = 26, HUM_BK_CLIP = 27,
     HUM_BK_MODE = 28,
-    /* 64-bit RNG stream key as two u32 halves; initialised to splitmix64(seed + lane_offset + lane) */
+    /* 64-bit RNG stream key as two u32 halves; initialised to splitmix64(splitmix64(seed) ^ (lane_offset + lane)) */
     HUM_BK_RNG_KEY_LO = 29, HUM_BK_RNG_KEY_HI = 30,
     /* hierarchical env only (hier_env.py): steps_remaining_at_level, num_high_level_steps, the agent expected
        to act next (1 = high), highTargetScore, cumulative_driftScore, driftScore, delta_highTargetScore,
@@ -110,7 +111,7 @@ typedef struct hum_config {
     int32_t solver_iters;     /* 5 */
     double erp_contact, erp_limit, mu_ground, mu_self, contact_thresh;
     double lin_damp, ang_damp, limit_max_impulse, max_coord_vel;
-    int32_t max_contacts;     /* 16 (cooperative kernel <= 16, per-lane kernel <= 24) */
+    int32_t max_contacts;     /* HUM_MAX_CONTACTS (default: every candidate, nothing dropped); lower = diagnostic cap */
     int32_t self_collision;   /* 1 */
     int32_t joint_damping;    /* 1 = implicit MJCF joint damping */
     int32_t kernel;           /* 1 = cooperative (16 lanes/env, LDS-resident; default), 0 = one env per lane */

@@ -131,7 +131,7 @@ def mass_matrix(state):
 
 def contacts(state, params=None):
     P = params or default_params()
-    out = np.zeros((64, 12))
+    out = np.zeros((95, 12))
     n = lib().om_contacts(ctypes.byref(P), _p(np.ascontiguousarray(state, dtype=np.float64)), _p(out))
     return out[:n]
 
@@ -157,20 +157,37 @@ def splitmix64(z):
     return z ^ (z >> 31)
 
 
-def lane_draw(seed, lane, counter, lo, hi):
-    """Counter-based per-lane integer draw in [lo, hi) (replaces the reference's unseeded
-    np.random.default_rng(), low_level_env.py:84; same definition as the product kernel)."""
-    k = splitmix64((seed + lane) & M64)
-    x = splitmix64((k + counter) & M64)
+def lane_key(seed, lane):
+    """64-bit stream key of global lane `lane` under `seed` (the product's init_kernel): non-additive, so
+    (seed s, lane i+1) and (seed s+1, lane i) are different streams."""
+    return splitmix64(splitmix64(seed & M64) ^ (lane & M64))
+
+
+def legacy_lane_key(seed, lane):
+    """Key of the round-1 derivation splitmix64(seed + lane): the golden fixtures' recorded draws were made
+    with it (tests inject it explicitly through the bookkeeping key words)."""
+    return splitmix64((seed + lane) & M64)
+
+
+def key_draw(key, counter, lo, hi):
+    """Counter-based integer draw in [lo, hi) from a lane key (Lemire range map of the high 32 bits)."""
+    x = splitmix64((key + counter) & M64)
     return lo + (((x >> 32) * (hi - lo)) >> 32)
 
 
+def lane_draw(seed, lane, counter, lo, hi):
+    """Counter-based per-lane integer draw in [lo, hi) (replaces the reference's unseeded
+    np.random.default_rng(), low_level_env.py:84; same definition as the product kernel)."""
+    return key_draw(lane_key(seed, lane), counter, lo, hi)
+
+
 class LaneRNG:
-    def __init__(self, seed, lane):
-        self.seed, self.lane, self.counter = seed, lane, 0
+    def __init__(self, seed=0, lane=0, key=None, counter=0):
+        self.key = lane_key(seed, lane) if key is None else key
+        self.counter = counter
 
     def integers(self, lo, hi):
-        v = lane_draw(self.seed, self.lane, self.counter, lo, hi)
+        v = key_draw(self.key, self.counter, lo, hi)
         self.counter += 1
         return int(v)
 

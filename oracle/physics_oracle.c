@@ -37,7 +37,9 @@
 #include "humanoid_links_gen.h"
 
 #define NV (6 + OM_ND)
-#define MAXC 64
+/* contact list capacity: every candidate fits (29 sphere / capsule-end ground points + 66 geom pairs = 95), so
+   the default max_contacts never truncates (Bullet has no global contact cap) */
+#define MAXC 95
 #define MAXROW (3 * MAXC + 2 * OM_ND)
 
 typedef struct {
@@ -547,7 +549,7 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
     for (int a = 0; a < NV; a++) nu[a] = clampd(nu[a], -P->max_coord_vel, P->max_coord_vel);
 
     /* 2. constraint rows */
-    static om_row rows[MAXROW];
+    om_row rows[MAXROW];   /* on the stack: the OpenMP batch driver steps lanes concurrently */
     int nr = 0;
     double H[NV * NV];
     mass_matrix(&K, H);
@@ -675,7 +677,7 @@ void om_default_params(om_params* P) {
     P->lin_damp = 0.04;
     P->ang_damp = 0.04;
     P->limit_max_impulse = 100.0;
-    P->max_contacts = 16;
+    P->max_contacts = MAXC;
     P->self_collision = 1;
     P->joint_damping = 1;
     P->max_coord_vel = 100.0;

@@ -186,7 +186,7 @@ def install_stubs():
 
 class RecordingRNG:
     def __init__(self, seed, lane):
-        self.r = O.LaneRNG(seed, lane)
+        self.r = O.LaneRNG(key=O.legacy_lane_key(seed, lane))   # the key the committed fixtures were made with
         self.log = []
 
     def integers(self, lo, hi):

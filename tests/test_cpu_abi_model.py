@@ -47,7 +47,7 @@ def test_config_layout_matches_header(tmp_path):
 def test_default_config_values():
     c = N.default_config()
     assert (c.dt_env, c.substeps, c.solver_iters, c.gravity) == (0.0165, 4, 5, 9.8)
-    assert abs(c.mu_ground - 1.6) < 1e-15 and c.erp_contact == 0.9 and c.max_contacts == 16 and c.kernel == 1
+    assert abs(c.mu_ground - 1.6) < 1e-15 and c.erp_contact == 0.9 and c.max_contacts == 95 and c.kernel == 1
     P = O.default_params()
     assert P.max_contacts == c.max_contacts and P.erp_limit == c.erp_limit and P.contact_thresh == c.contact_thresh
     assert P.limit_max_impulse == c.limit_max_impulse and P.max_coord_vel == c.max_coord_vel
@@ -171,14 +171,17 @@ def test_clip_shapes_and_known_answers():
 
 
 def test_rng_definition():
-    """Counter-based lane RNG: deterministic, in range, distinct per lane; key = splitmix64(seed + lane)."""
+    """Counter-based lane RNG: deterministic, in range, distinct per lane;
+    key = splitmix64(splitmix64(seed) ^ lane) (non-additive: seed s lane i+1 != seed s+1 lane i)."""
     vals = [O.lane_draw(7, 3, c, -180, 180) for c in range(2000)]
     assert min(vals) >= -180 and max(vals) < 180 and len(set(vals)) > 300
     assert O.lane_draw(7, 3, 5, 0, 293) == O.lane_draw(7, 3, 5, 0, 293)
     assert [O.lane_draw(0, l, 0, 0, 1000) for l in range(8)] != [O.lane_draw(0, 0, 0, 0, 1000)] * 8
-    key = O.splitmix64(7 + 3)
+    key = O.splitmix64(O.splitmix64(7) ^ 3)
     x = O.splitmix64((key + 5) & O.M64)
     assert O.lane_draw(7, 3, 5, -180, 180) == -180 + (((x >> 32) * 360) >> 32)
+    # streams of neighbouring (seed, lane) pairs do not coincide (the additive key made them equal)
+    assert [O.lane_draw(7, 4, c, 0, 1 << 30) for c in range(8)] != [O.lane_draw(8, 3, c, 0, 1 << 30) for c in range(8)]
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):

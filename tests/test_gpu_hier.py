@@ -37,7 +37,7 @@ def golden_hier():
 def book_rows(r):
     """HUM_NBOOK rows with the reference bookkeeping BEFORE each recorded call."""
     seed, lane, _, debug, _, _, _ = [int(x) for x in r["meta"]]
-    key = O.splitmix64((seed + lane) & O.M64)
+    key = O.legacy_lane_key(seed, lane)   # the stream the fixtures' recorded draws came from
     T = len(r["done"])
     out = np.zeros((T, N.HUM_NBOOK))
     for t in range(T):

@@ -39,7 +39,7 @@ SCEN = ["motion02_04_l0", "motion02_04_l1", "motion02_04_l2", "motion08_03_l0", 
 def book_rows(r, t_idx):
     """HUM_NBOOK rows holding the reference bookkeeping BEFORE each step t in t_idx."""
     seed, lane, _, debug, _, _, _ = [int(x) for x in r["meta"]]
-    key = O.splitmix64((seed + lane) & O.M64)
+    key = O.legacy_lane_key(seed, lane)   # the stream the fixtures' recorded draws came from
     out = np.zeros((len(t_idx), N.HUM_NBOOK))
     for row, t in enumerate(t_idx):
         src = (lambda k: r["book0_" + k]) if t == 0 else (lambda k: r["book_" + k][t - 1])
