@@ -85,6 +85,7 @@ KArgs make_args(hum_env* e) {
     a.P.joint_damping = c.joint_damping;
     a.P.lds_rows = lds_rows_of(c);
     a.hier = c.hier;
+    a.np1 = c.numpy_semantics == HUM_NUMPY_1;
     a.clips = e->clips_dev;
     a.pred = e->pred;
     a.npred = e->npred;
@@ -104,7 +105,20 @@ bool any_clip(hum_env* e) {
 }
 }  // namespace
 
-namespace { int launch_step(hum_env* e, const KArgs& a, hipStream_t s); }
+namespace {
+int launch_step(hum_env* e, const KArgs& a, hipStream_t s);
+// Inputs a captured step graph holds by value (clip descriptors, predefined course) are about to change:
+// finish every launch that may read the old ones, then drop the graph so the next hum_step_graph recaptures.
+hipError_t quiesce(hum_env* e) {
+    hipError_t st = hipStreamSynchronize(e->stream);
+    if (st == hipSuccess) st = hipDeviceSynchronize();   // launches on caller streams (hum_step(.., stream))
+    if (e->graph) {
+        (void)hipGraphExecDestroy(e->graph);
+        e->graph = nullptr;
+    }
+    return st;
+}
+}  // namespace
 
 extern "C" {
 
@@ -139,6 +153,7 @@ void hum_default_config(hum_config* c) {
     c->hier = 0;
     c->envs_per_block = 4;
     c->lds_rows = 0;
+    c->numpy_semantics = HUM_NUMPY_1;
 }
 
 int hum_create(const hum_config* cfg, hum_env** out) {
@@ -153,6 +168,8 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     if (cfg->envs_per_block != 1 && cfg->envs_per_block != 2 && cfg->envs_per_block != 4)
         return fail(HUM_ERR_ARG, "hum_create: envs_per_block must be 1, 2 or 4");
     if (cfg->lds_rows < 0) return fail(HUM_ERR_ARG, "hum_create: lds_rows must be >= 0");
+    if (cfg->numpy_semantics != HUM_NUMPY_1 && cfg->numpy_semantics != HUM_NUMPY_2)
+        return fail(HUM_ERR_ARG, "hum_create: numpy_semantics must be HUM_NUMPY_1 or HUM_NUMPY_2");
     static_assert(MAXC_G == HUM_MAX_CONTACTS && MAXC == HUM_MAX_CONTACTS, "contact list holds every candidate");
     if (cfg->max_contacts < 0 || cfg->max_contacts > HUM_MAX_CONTACTS)
         return fail(HUM_ERR_ARG, "hum_create: max_contacts out of range [0, HUM_MAX_CONTACTS]");
@@ -217,6 +234,7 @@ int hum_set_clip(hum_env* e, int32_t id, const double* pos, int32_t n_pos, const
     if (!e || id < 0 || id >= HUM_MAX_CLIPS || !pos || !vel || !rel || !ep) return fail(HUM_ERR_ARG, "hum_set_clip: bad argument");
     if (n_pos < 8 || n_vel < 1 || n_rel < n_pos || n_ep < n_pos) return fail(HUM_ERR_ARG, "hum_set_clip: inconsistent table sizes");
     HIPCHK(hipSetDevice(e->cfg.device));
+    HIPCHK(quiesce(e));
     if (e->clip_dev[id]) HIPCHK(hipFree(e->clip_dev[id]));
     const size_t np = (size_t)n_pos * 14, nv = (size_t)n_vel * 14, nr = (size_t)n_rel * 14, ne = (size_t)n_ep * 27;
     double* buf;
@@ -238,6 +256,7 @@ int hum_set_lane_clips(hum_env* e, const int32_t* clip_of_lane) {
         if (clip_of_lane[i] < 0 || clip_of_lane[i] >= HUM_MAX_CLIPS || !e->clip_set[clip_of_lane[i]])
             return fail(HUM_ERR_NOCLIP, "hum_set_lane_clips: lane refers to a clip that was not uploaded");
     HIPCHK(hipSetDevice(e->cfg.device));
+    HIPCHK(quiesce(e));   // in-flight launches (or graph replays) read the clip column
     HIPCHK(hipMemcpy(e->d.bi + 3 * e->n, clip_of_lane, e->n * sizeof(int), hipMemcpyHostToDevice));
     return HUM_OK;
 }
@@ -245,6 +264,7 @@ int hum_set_lane_clips(hum_env* e, const int32_t* clip_of_lane) {
 int hum_set_lane_modes(hum_env* e, const uint32_t* modes) {
     if (!e || !modes) return fail(HUM_ERR_ARG, "hum_set_lane_modes: null argument");
     HIPCHK(hipSetDevice(e->cfg.device));
+    HIPCHK(quiesce(e));
     HIPCHK(hipMemcpy(e->d.bi + 5 * e->n, modes, e->n * sizeof(int), hipMemcpyHostToDevice));
     return HUM_OK;
 }
@@ -252,6 +272,7 @@ int hum_set_lane_modes(hum_env* e, const uint32_t* modes) {
 int hum_set_predefined_targets(hum_env* e, const double* xyz, int32_t n) {
     if (!e || (n > 0 && !xyz) || n < 0) return fail(HUM_ERR_ARG, "hum_set_predefined_targets: bad argument");
     HIPCHK(hipSetDevice(e->cfg.device));
+    HIPCHK(quiesce(e));   // a captured graph holds pred / npred by value
     if (e->pred) HIPCHK(hipFree(e->pred));
     e->pred = nullptr;
     e->npred = n;

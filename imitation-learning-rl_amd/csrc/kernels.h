@@ -57,6 +57,7 @@ struct KArgs {
     float* aux;
     // hierarchical env (hum_hier_step / hum_hier_reset)
     int hier;
+    int np1;                        // hum_config.numpy_semantics == HUM_NUMPY_1: float64 scalar promotion
     const float* act_high;          // [n,2]
     const unsigned char* agent_sel; // [n] 1 = high, 0 = low (NULL = the lane's expected agent)
     unsigned char* agents;          // [n] HUM_AGENT_* present in the returned dicts
@@ -64,6 +65,17 @@ struct KArgs {
     float* rew_high;                // [n]
     float* obs_high_reset;          // [n,44]
 };
+
+// CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
+// np.clip(a, -1, 1)) - a float32 product under NumPy >= 2 (NEP 50), float64 under NumPy 1.x
+__device__ inline double motor_torque(bool np1, float gain_f, double gain_d, float act) {
+    const float c = fminf(fmaxf(act, -1.f), 1.f);
+    return np1 ? gain_d * (double)c : (double)(gain_f * c);
+}
+// calcAliveReward (low_level_env.py:384-387): cur_obs[0] (float32) + initial_z 0.8 > 0.75, same promotion rule
+__device__ inline double alive_reward(bool np1, float obs0) {
+    return (np1 ? ((double)obs0 + 0.8) > 0.75 : (obs0 + 0.8f) > 0.75f) ? 2.0 : -1.0;
+}
 
 // ----------------------------------------------------------------------------------- SoA lane I/O
 __device__ inline void load_book(const KArgs& a, int i, Book& b) {
@@ -224,7 +236,7 @@ __device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* ac
         b.es = -1.0 * (double)run + -0.1 * (double)stall;
     }
     b.jls = -0.1 * jal;
-    b.alive = ((obs[0] + 0.8f) > 0.75f) ? 2.0 : -1.0;
+    b.alive = alive_reward(a.np1, obs[0]);
     b.bps = posture;
     double total = 0;
     total = total + b.dj * REWARD_W[0];
@@ -435,7 +447,7 @@ __device__ void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsi
             b.es = -1.0 * (double)run + -0.1 * (double)stall;
         }
         b.jls = -0.1 * jal;
-        b.alive = ((obs[0] + 0.8f) > 0.75f) ? 2.0 : -1.0;
+        b.alive = alive_reward(a.np1, obs[0]);
         b.cum_alive = b.cum_alive + b.alive;
         b.bps = posture;
         {                                                                                   // calcDriftScore :461-467
@@ -544,7 +556,12 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
     Book b;
     load_lane(a, i, st, b);
     unsigned ef = 0;
-    // hierarchical env: the lane's acting agent (step(action_dict) dispatch, hier_env.py:363-366)
+    // hierarchical env: the lane's acting agent (step(action_dict) dispatch, hier_env.py:363-366); a lane with
+    // no action this round (HUM_AGENT_SEL_SKIP) is left untouched and reports no agent
+    if (a.hier && a.agent_sel && a.agent_sel[i] == HUM_AGENT_SEL_SKIP) {
+        a.agents[i] = 0;
+        return;
+    }
     const bool high = a.hier && (a.agent_sel ? a.agent_sel[i] != 0 : b.expect_high != 0);
     float act[HUM_NACT];
     bool finite = true;
@@ -562,10 +579,8 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && !high) {
         T tau[NDOF];
 #pragma unroll
-        for (int k = 0; k < HUM_NACT; k++) {   // apply_action: float(1 * power * 0.41 * clip(a)) in float32
-            const float g = (float)act_gain[k];
-            tau[act_dof[k]] = (T)(double)(g * fminf(fmaxf(act[k], -1.f), 1.f));
-        }
+        for (int k = 0; k < HUM_NACT; k++)   // apply_action
+            tau[act_dof[k]] = (T)motor_torque(a.np1, (float)act_gain[k], act_gain[k], act[k]);
         Lane<T> rows{(T*)a.scratch + i, (long)a.n};
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++) {
@@ -604,16 +619,18 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     for (int e = l; e < HUM_NSTATE; e += GL)
         S.st[e] = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
     bool fin = true;
-    for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60), float32 product
+    for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60)
         const float av = valid ? a.act[(long)i * HUM_NACT + k] : 0.f;
         fin = fin && isfinite(av);
-        S.tau[M.act_dof[k]] = (T)(double)(M.act_gain[k] * fminf(fmaxf(isfinite(av) ? av : 0.f, -1.f), 1.f));
+        S.tau[M.act_dof[k]] = (T)motor_torque(a.np1, M.act_gain[k], M.act_gain_d[k], isfinite(av) ? av : 0.f);
     }
     const int gbit = (threadIdx.x & 63) & ~(GL - 1);
     // hierarchical env: envs whose acting agent is the high level take no physics step (hier_env.py:538-571)
-    const bool high = a.hier && valid && (a.agent_sel ? a.agent_sel[i] != 0 : a.bi[10 * a.n + i] != 0);
+    const unsigned char sel = a.hier && valid && a.agent_sel ? a.agent_sel[i] : (unsigned char)0;
+    const bool skip = a.hier && valid && a.agent_sel && sel == HUM_AGENT_SEL_SKIP;   // no action: lane untouched
+    const bool high = a.hier && valid && !skip && (a.agent_sel ? sel != 0 : a.bi[10 * a.n + i] != 0);
     const bool env_ok = high || ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
-    const bool any_phys = __ballot(valid && !high) != 0;   // wave-uniform
+    const bool any_phys = __ballot(valid && !high && !skip) != 0;   // wave-uniform
     __syncthreads();
     unsigned ef = 0;
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
@@ -635,7 +652,9 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     Book b;
     T st[HUM_NSTATE];
     bool rst = false;
-    if (valid && l == 0) {
+    if (valid && l == 0 && skip) {
+        a.agents[i] = 0;
+    } else if (valid && l == 0) {
         load_book(a, i, b);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
@@ -735,6 +754,14 @@ __global__ void __launch_bounds__(256) reset_kernel(KArgs a) {
     float obs[HUM_NOBS];
     const int sf = a.start_frame ? a.start_frame[i] : -1;
     const double ry = a.reset_yaw ? a.reset_yaw[i] : 0.0;
+    {   // resetFromFrame past the clip: the reference's DataFrame.iloc raises IndexError (low_level_env.py:208,
+        // :282-291; hier_env.py:293-304 also reads end-point row startFrame + 1)
+        const ClipDev& c = a.clips[b.clip];
+        if (sf >= (a.hier ? c.n_pos - 1 : c.n_pos)) {
+            atomicOr(a.eflags, HUM_EFLAG_BAD_START_FRAME);
+            return;
+        }
+    }
     if (a.hier) {
         hier_reset_lane(a, i, st, b, sf, ry, obs, ef);
         if (a.obs_high) {
@@ -761,6 +788,39 @@ static __global__ void init_kernel(KArgs a) {   // fresh lanes: clip 0, no mode,
     a.bi[7 * a.n + i] = (int)(unsigned)(k >> 32);
 }
 
+// calcEndPointScore (low_level_env.py:361-382): sum over {link0_11: RightLeg 1, right_foot: RightFoot 3,
+// link0_18: LeftLeg 1, left_foot: LeftFoot 3} of w * |starting_ep_pos + Rz(highLevelDegTarget) ref - part|,
+// score = -sum / 8 (useExp: exp(3 score)); scipy's from_euler('z') matrix and apply() order, float64
+#pragma clang fp contract(off)
+template <typename T>
+__device__ inline void end_point_score(const KArgs& a, const T* st, const Book& b, double& score, double& score_exp) {
+    const ClipDev& c = a.clips[b.clip];
+    Kin<T> K;
+    forward_kinematics(st + 3, st + 13, K);
+    T pp[NPART][3];
+    part_positions(K, pp);
+    const double qz = sin(b.hldt / 2), qw = cos(b.hldt / 2);
+    const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw);
+    const double r11 = -(qz * qz) + qw * qw, r22 = qz * qz + qw * qw;
+    constexpr int PART[4] = {10, 12, 17, 19}, EPC[4] = {6, 9, 0, 3};   // link0_11, right_foot, link0_18, left_foot
+    constexpr double W[4] = {1, 3, 1, 3};
+    const double* e = c.ep + b.frame * 27;
+    double d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const double x = e[EPC[k]], y = e[EPC[k] + 1], z = e[EPC[k] + 2];
+        const double v2x = b.sep[0] + ((r00 * x + r01 * y) + 0.0 * z);
+        const double v2y = b.sep[1] + ((r10 * x + r11 * y) + 0.0 * z);
+        const double v2z = b.sep[2] + ((0.0 * x + 0.0 * y) + r22 * z);
+        const double v1x = (double)st[0] + (double)pp[PART[k]][0], v1y = (double)st[1] + (double)pp[PART[k]][1];
+        const double v1z = (double)st[2] + (double)pp[PART[k]][2];
+        d = d + norm3_blas(v2x - v1x, v2y - v1y, v2z - v1z) * W[k];
+    }
+    score = -d / 8;
+    score_exp = exp(3 * score);
+}
+#pragma clang fp contract(on)
+
 template <typename T>
 __global__ void aux_kernel(KArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -781,6 +841,11 @@ __global__ void aux_kernel(KArgs a) {
     o[HUM_AUX_ELECTRICITY] = (float)b.es;
     o[HUM_AUX_JOINT_LIMIT] = (float)b.jls;
     o[HUM_AUX_DIST_FROM_ORIGIN] = (float)norm3_blas(b.robot_pos[0], b.robot_pos[1], b.robot_pos[2]);
+    double sc, sce;
+    end_point_score(a, st, b, sc, sce);
+    o[HUM_AUX_END_POINT_SCORE] = (float)sc;
+    o[HUM_AUX_END_POINT_SCORE_EXP] = (float)sce;
+    for (int k = 0; k < 3; k++) o[HUM_AUX_ROBOT_POS + k] = (float)b.robot_pos[k];
 }
 
 template <typename T>

@@ -54,6 +54,7 @@ struct ModelTab {
     T gbr[NGEOM];                        // bounding-sphere radius about the segment midpoint: |p2-p1|/2 + r
     int act_dof[NACT];
     float act_gain[NACT];
+    double act_gain_d[NACT];
 };
 __device__ inline int cand_a(int v) { return v & 0xffff; }
 __device__ inline int cand_b(int v) { return v >> 16; }
@@ -215,7 +216,7 @@ constexpr ModelTab<T> make_tab() {
         for (int e = 0; e < (geom_type[g] == 0 ? 1 : 2); e++) { m.cand[c] = g | (int)((unsigned)(-1 - e) << 16); c++; }
     }
     for (int k = 0; k < NPAIR; k++) { m.cand[c] = pair_a[k] | (pair_b[k] << 16); c++; }
-    for (int k = 0; k < NACT; k++) { m.act_dof[k] = hm::act_dof[k]; m.act_gain[k] = (float)hm::act_gain[k]; }
+    for (int k = 0; k < NACT; k++) { m.act_dof[k] = hm::act_dof[k]; m.act_gain[k] = (float)hm::act_gain[k]; m.act_gain_d[k] = hm::act_gain[k]; }
     return m;
 }
 

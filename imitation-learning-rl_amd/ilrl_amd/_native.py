@@ -8,13 +8,15 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
-HUM_ABI_VERSION = 4   # include/humanoid_env.h
-HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 12
+HUM_ABI_VERSION = 5   # include/humanoid_env.h
+HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
-HUM_AGENT_HIGH, HUM_AGENT_LOW = 1, 2
+HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
 HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS = 1, 2
 HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
-HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW = 1, 2, 4
+HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW, HUM_EFLAG_BAD_START_FRAME = 1, 2, 4, 8
+HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
+HUM_MAX_CONTACTS = 95
 
 # bookkeeping layout (HUM_BK_*)
 BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, target=4, starting_robot_pos=7,
@@ -25,7 +27,8 @@ BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, targe
           steps_remaining_at_level=31, num_high_level_steps=32, expect_high=33, highTargetScore=34,
           cumulative_driftScore=35, driftScore=36, delta_highTargetScore=37, cumulative_aliveReward=38, body_xy=39)
 AUX = ["deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bodyPostureScore", "highTargetScore",
-       "driftScore", "baseReward", "aliveReward", "electricityScore", "jointLimitScore", "dist_from_origin"]
+       "driftScore", "baseReward", "aliveReward", "electricityScore", "jointLimitScore", "dist_from_origin",
+       "endPointScore", "endPointScoreExp", "robot_pos_x", "robot_pos_y", "robot_pos_z"]
 
 # every symbol include/humanoid_env.h declares
 EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_create", "hum_destroy", "hum_set_clip",
@@ -44,7 +47,8 @@ class HumConfig(ctypes.Structure):
                 ("limit_max_impulse", ctypes.c_double), ("max_coord_vel", ctypes.c_double),
                 ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
                 ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32),
-                ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32), ("lds_rows", ctypes.c_int32)]
+                ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32), ("lds_rows", ctypes.c_int32),
+                ("numpy_semantics", ctypes.c_int32)]
 
 
 class NativeError(RuntimeError):

@@ -13,10 +13,12 @@
 
 ray is optional (absent in this image): BaseEnv is subclassed only when importable.
 """
+import secrets
+
 import numpy as np
 
 from . import _native as N
-from .low_level_env import _box, _BookView
+from .low_level_env import _box, _BookView, _optional_base, env_seed
 from .vec_env import HumanoidVecEnv, _ptr
 
 ENV_HIER = "HumanoidBulletEnv-v0-Hier"
@@ -94,8 +96,11 @@ class HierarchicalHumanoidEnv(_HierBookView):
 
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 60}
 
-    def __init__(self, customRobot=None, seed=0, device=0, precision="fp32", **physics):
-        self.__dict__["_v"] = HierVecEnv(1, seed=seed, device=device, precision=precision, **physics)
+    def __init__(self, customRobot=None, seed=None, device=0, precision="fp32", lane_offset=0, **physics):
+        if seed is None:   # the reference's unseeded default_rng() (hier_env.py:89)
+            seed = secrets.randbits(63)
+        self.__dict__["_v"] = HierVecEnv(1, seed=seed, device=device, lane_offset=lane_offset, precision=precision,
+                                         **physics)
         self.__dict__["_cache"] = None
         self.__dict__["_debug"] = False
         self.__dict__["_pred_on"] = False
@@ -186,15 +191,7 @@ class HierLaneView(_HierBookView):
         return self._venv._books()[self._i]
 
 
-def _base_env_cls():
-    try:
-        from ray.rllib.env.base_env import BaseEnv
-        return BaseEnv
-    except Exception:
-        return object
-
-
-class HierarchicalVectorEnv(_base_env_cls()):
+class HierarchicalVectorEnv(_optional_base("ray.rllib.env.base_env", "BaseEnv")):
     """RLlib 1.2 BaseEnv over N hierarchical lanes (one hum_hier_step launch per send_actions/poll round).
 
     poll() -> (obs, rewards, dones, infos, off_policy_actions) as {env_id: {agent_id: ...}} with
@@ -202,8 +199,11 @@ class HierarchicalVectorEnv(_base_env_cls()):
     launch and try_reset(env_id) serves the reset observation {"high_level_agent": obs}.
     """
 
-    def __init__(self, num_envs, seed=0, device=0, precision="fp32", **physics):
-        self.venv = HierVecEnv(num_envs, seed=seed, device=device, precision=precision, **physics)
+    def __init__(self, num_envs, seed=None, device=0, precision="fp32", lane_offset=0, **physics):
+        if seed is None:
+            seed = secrets.randbits(63)
+        self.venv = HierVecEnv(num_envs, seed=seed, device=device, lane_offset=lane_offset, precision=precision,
+                               **physics)
         self.num_envs = num_envs
         self._views = [HierLaneView(self, i) for i in range(num_envs)]
         self._book_cache = None
@@ -232,10 +232,11 @@ class HierarchicalVectorEnv(_base_env_cls()):
         return obs, rew, dones, infos, {}
 
     def send_actions(self, action_dict):
+        """Lanes absent from action_dict (RLlib did not act on them) are left unstepped (HUM_AGENT_SEL_SKIP)."""
         n = self.num_envs
         ah = np.zeros((n, 2), np.float32)
         al = np.zeros((n, 17), np.float32)
-        agent = np.zeros(n, np.uint8)
+        agent = np.full(n, N.HUM_AGENT_SEL_SKIP, np.uint8)
         for i, ad in action_dict.items():
             assert len(ad) == 1, ad
             if HIGH in ad:
@@ -243,6 +244,7 @@ class HierarchicalVectorEnv(_base_env_cls()):
                 agent[i] = 1
             else:
                 al[i] = list(ad.values())[0]
+                agent[i] = 0
         if not np.isfinite(al).all():
             raise AssertionError("non-finite action (humanoid.py:55)")
         agents, oh, ol, rh, rl, done, _ = [x.cpu().numpy() for x in
@@ -279,8 +281,17 @@ class HierarchicalVectorEnv(_base_env_cls()):
 
 
 def make_env_hier(env_config=None):
-    """train_config.py:18-20 (env_config ignored like the reference)."""
-    return HierarchicalHumanoidEnv()
+    """train_config.py:18-20; each env gets its own RNG stream (low_level_env.env_seed)."""
+    seed, off = env_seed(env_config, 1)
+    return HierarchicalHumanoidEnv(seed=seed, lane_offset=off)
+
+
+def make_env_hier_vec(env_config=None):
+    """One N-lane BaseEnv per RLlib worker (env_config["num_lanes"], default 1024)."""
+    cfg = env_config if env_config is not None else {}
+    n = int(cfg.get("num_lanes", 1024)) if hasattr(cfg, "get") else 1024
+    seed, off = env_seed(env_config, n)
+    return HierarchicalVectorEnv(n, seed=seed, lane_offset=off)
 
 
 def register_envs():

@@ -6,16 +6,45 @@
 * `HumanoidVectorEnv`    - RLlib-1.2 VectorEnv protocol (vector_reset / reset_at / vector_step /
   get_unwrapped) over N lanes of ONE kernel launch per step; get_unwrapped() returns lane views with the
   attributes RewardLogCallback reads (custom_callback.py:43-80).
-* `make_env_low`, `register_envs` - the registration contract of train_config.py:13-15,29,320-321.
+* `make_env_low`, `make_env_low_vec`, `register_envs` - the registration contract of train_config.py:13-15,29,
+  320-321: `make_env_low` returns the single-env gym view (one lane per env, the reference's shape);
+  `make_env_low_vec` returns ONE N-lane `HumanoidVectorEnv` per RLlib worker, which RLlib uses as the worker's
+  vector env directly (BaseEnv.to_base_env recognises VectorEnv subclasses), so a sampler step is one launch.
 
-gym and ray are optional imports (absent in this image); the spaces fall back to a minimal Box.
+gym and ray are optional imports (absent in this image): `LowLevelHumanoidEnv` subclasses gym.Env and
+`HumanoidVectorEnv` subclasses ray.rllib.env.vector_env.VectorEnv when those import; the spaces fall back to
+a minimal Box.
 """
+import secrets
+
 import numpy as np
 
 from . import _native as N
 from .vec_env import HumanoidVecEnv
 
 ENV_LOW = "HumanoidBulletEnv-v0-Low"
+
+
+def _optional_base(module, name):
+    try:
+        mod = __import__(module, fromlist=[name])
+        return getattr(mod, name)
+    except Exception:
+        return object
+
+
+def env_seed(env_config=None, n_lanes=1):
+    """(seed, lane_offset) for an env built by a registration creator.  The reference draws from an unseeded
+    np.random.default_rng() per env (low_level_env.py:84), so copies never share a stream: an explicit
+    env_config["seed"] is honoured, RLlib's worker_index / vector_index give each copy its own global lanes,
+    and without a seed the job seed comes from OS entropy."""
+    cfg = env_config if env_config is not None else {}
+    seed = cfg.get("seed") if hasattr(cfg, "get") else None
+    if seed is None:
+        seed = secrets.randbits(63)
+    worker = int(getattr(cfg, "worker_index", 0) or 0)
+    vector = int(getattr(cfg, "vector_index", 0) or 0)
+    return int(seed), (worker * 4096 + vector) * int(n_lanes)
 
 
 def _box(low, high, shape):
@@ -64,17 +93,19 @@ class _BookView:
         raise AttributeError(name)
 
 
-class LowLevelHumanoidEnv(_BookView):
+class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
     """Single-env view (n = 1 lane) with the reference signature (low_level_env.py:39)."""
 
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 60}
 
-    def __init__(self, reference_name="motion08_03", useCustomEnv=False, customRobot=None, seed=0, device=0,
-                 precision="fp32", **physics):
+    def __init__(self, reference_name="motion08_03", useCustomEnv=False, customRobot=None, seed=None, device=0,
+                 precision="fp32", lane_offset=0, **physics):
         if useCustomEnv:
             raise NotImplementedError("useCustomEnv (heightfield terrain, humanoid.py:68-188) is out of scope")
+        if seed is None:   # the reference's unseeded default_rng() (:84): a fresh stream per env
+            seed = secrets.randbits(63)
         self.__dict__["_v"] = HumanoidVecEnv(1, clips=(reference_name,), seed=seed, device=device,
-                                             precision=precision, **physics)
+                                             lane_offset=lane_offset, precision=precision, **physics)
         self.__dict__["_cache"] = None
         self.__dict__["_debug"] = False
         self.__dict__["_pred_on"] = False
@@ -124,6 +155,8 @@ class LowLevelHumanoidEnv(_BookView):
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :247-305
         if not (startFromRef and initVel):
             raise NotImplementedError("resetFromFrame supports startFromRef=True, initVel=True (all reference callers)")
+        if not 0 <= int(startFrame) < self.max_frame + 1:   # DataFrame.iloc (:208) raises past the table
+            raise IndexError("single positional indexer is out-of-bounds (startFrame=%d)" % int(startFrame))
         return self._obs(self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw)))
 
     def step(self, action, debug=False):                                # :322-323, :475-526
@@ -143,8 +176,18 @@ class LowLevelHumanoidEnv(_BookView):
         raise NotImplementedError("rendering is out of scope (env_vis_low.py)")
 
 
+# RewardLogCallback attributes (custom_callback.py:43-80) served from the device aux row of ONE lane
+_AUX_ATTR = {"deltaJoints": "deltaJoints", "deltaEndPoints": "deltaEndPoints", "lowTargetScore": "lowTargetScore",
+             "deltaVelJoints": "deltaVelJoints", "bodyPostureScore": "bodyPostureScore",
+             "highTargetScore": "highTargetScore", "driftScore": "driftScore", "baseReward": "baseReward",
+             "aliveReward": "aliveReward", "electricityScore": "electricityScore",
+             "jointLimitScore": "jointLimitScore"}
+
+
 class LaneView(_BookView):
-    """get_unwrapped()[i] of HumanoidVectorEnv: reference attribute names for lane i."""
+    """get_unwrapped()[i] of HumanoidVectorEnv: reference attribute names for lane i.  The callback terms and
+    robot_pos come from lane i's row of hum_get_aux (one small device->host copy per step, cached); the other
+    bookkeeping attributes (frame, target, ...) from a full state read."""
 
     def __init__(self, venv, i):
         self.__dict__["_venv"] = venv
@@ -153,22 +196,37 @@ class LaneView(_BookView):
     def _book(self):
         return self._venv._books()[self._i]
 
+    def __getattr__(self, name):
+        if name in _AUX_ATTR:
+            return float(self._venv._aux_row(self._i)[N.AUX.index(_AUX_ATTR[name])])
+        if name == "robot_pos":
+            k = N.AUX.index("robot_pos_x")
+            return self._venv._aux_row(self._i)[k:k + 3].astype(np.float64)
+        return _BookView.__getattr__(self, name)
 
-class HumanoidVectorEnv:
-    """RLlib 1.2 `VectorEnv` protocol over N lanes (one kernel launch per vector_step).
+
+class HumanoidVectorEnv(_optional_base("ray.rllib.env.vector_env", "VectorEnv")):
+    """RLlib 1.2 `VectorEnv` over N lanes (one kernel launch per vector_step); a subclass of RLlib's VectorEnv
+    when ray imports, so `BaseEnv.to_base_env` drives it directly.
 
     vector_step returns the terminal observation for done lanes (gym semantics); the sampler then calls
     reset_at(i), which is served from the auto-reset buffer the same launch already filled.
     """
 
-    def __init__(self, num_envs, reference_name="motion09_03", seed=0, device=0, precision="fp32",
-                 clips=None, **physics):
+    def __init__(self, num_envs, reference_name="motion09_03", seed=None, device=0, precision="fp32",
+                 clips=None, lane_offset=0, **physics):
         clips = clips or (reference_name,)
-        self.venv = HumanoidVecEnv(num_envs, clips=clips, seed=seed, device=device, precision=precision, **physics)
+        if seed is None:
+            seed = secrets.randbits(63)
+        self.venv = HumanoidVecEnv(num_envs, clips=clips, seed=seed, device=device, lane_offset=lane_offset,
+                                   precision=precision, **physics)
         self.num_envs = num_envs
         self.observation_space = OBS_SPACE()
         self.action_space = ACT_SPACE()
+        if type(self).__mro__[1] is not object:   # ray's VectorEnv.__init__(observation_space, action_space, n)
+            super().__init__(self.observation_space, self.action_space, num_envs)
         self._book_cache = None
+        self._aux_rows = {}
         self._reset_obs = None
         self._views = [LaneView(self, i) for i in range(num_envs)]
 
@@ -177,9 +235,20 @@ class HumanoidVectorEnv:
             self._book_cache = self.venv.get_state()[1]
         return self._book_cache
 
+    def _aux_row(self, i):
+        if i not in self._aux_rows:
+            if not self._aux_rows:
+                self.venv.get_aux()
+            self._aux_rows[i] = self.venv.aux[i].cpu().numpy()
+        return self._aux_rows[i]
+
+    def _invalidate(self):
+        self._book_cache = None
+        self._aux_rows = {}
+
     def vector_reset(self):
         obs = self.venv.reset().cpu().numpy()
-        self._book_cache = None
+        self._invalidate()
         return [o for o in obs]
 
     def reset_at(self, index):
@@ -189,7 +258,7 @@ class HumanoidVectorEnv:
         mask = np.zeros(self.num_envs, dtype=np.uint8)
         mask[index] = 1
         obs = self.venv.reset(mask=mask)[index].cpu().numpy()
-        self._book_cache = None
+        self._invalidate()
         return obs
 
     def vector_step(self, actions):
@@ -200,7 +269,7 @@ class HumanoidVectorEnv:
             raise AssertionError("non-finite action (humanoid.py:55)")
         self._reset_obs = self.venv.obs_reset.cpu().numpy()
         self._reset_pending = d.copy()
-        self._book_cache = None
+        self._invalidate()
         return [x for x in o], [float(x) for x in r], [bool(x) for x in d], [{} for _ in range(self.num_envs)]
 
     def get_unwrapped(self):
@@ -211,12 +280,24 @@ class HumanoidVectorEnv:
 
 
 def make_env_low(env_config=None):
-    """train_config.py:13-15 (clip motion09_03; env_config ignored like the reference)."""
-    return LowLevelHumanoidEnv(reference_name="motion09_03")
+    """train_config.py:13-15: one single-lane env per call (clip motion09_03), each with its own RNG stream
+    (env_seed: env_config["seed"] / RLlib worker and vector index, else OS entropy)."""
+    seed, off = env_seed(env_config, 1)
+    return LowLevelHumanoidEnv(reference_name="motion09_03", seed=seed, lane_offset=off)
 
 
-def register_envs():
-    """register_env(ENV_LOW, make_env_low) (train_config.py:321) when Ray is importable."""
+def make_env_low_vec(env_config=None):
+    """One N-lane VectorEnv per RLlib worker (env_config["num_lanes"], default 1024; clip motion09_03): RLlib
+    uses a VectorEnv as the worker's vector env as-is, so every sampler step is one kernel launch."""
+    cfg = env_config if env_config is not None else {}
+    n = int(cfg.get("num_lanes", 1024)) if hasattr(cfg, "get") else 1024
+    seed, off = env_seed(env_config, n)
+    return HumanoidVectorEnv(n, reference_name="motion09_03", seed=seed, lane_offset=off)
+
+
+def register_envs(vectorised=True):
+    """register_env(ENV_LOW, ...) (train_config.py:321) when Ray is importable: the N-lane vector env per worker
+    (default), or the reference's one-env-per-call creator."""
     from ray.tune.registry import register_env
-    register_env(ENV_LOW, make_env_low)
+    register_env(ENV_LOW, make_env_low_vec if vectorised else make_env_low)
     return ENV_LOW

@@ -34,14 +34,14 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 4
+#define HUM_ABI_VERSION 5
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
 #define HUM_NBOOK 48    /* bookkeeping doubles per lane, layout HUM_BK_* below */
 #define HUM_NOBS_HIGH 44   /* high_level_obs_space shape, hier_env.py:52 */
 #define HUM_NACT_HIGH 2    /* high_level_act_space shape (cos, sin of the heading), hier_env.py:53-55 */
-#define HUM_NAUX 12     /* RewardLogCallback terms per lane, layout HUM_AUX_* below */
+#define HUM_NAUX 17     /* RewardLogCallback terms + calcEndPointScore + robot_pos per lane, HUM_AUX_* below */
 #define HUM_MAX_CLIPS 8
 #define HUM_MAX_CONTACTS 95  /* every contact candidate: 29 sphere / capsule-end ground points + 66 geom pairs */
 
@@ -64,6 +64,8 @@ extern "C" {
 #define HUM_EFLAG_NONFINITE_ACTION 1u   /* humanoid.py:55 assert np.isfinite(a).all(): lane not stepped */
 #define HUM_EFLAG_VEL_ROW 2u            /* frame beyond the velocity table (motion13_13): clamped row used */
 #define HUM_EFLAG_CONTACT_OVERFLOW 4u   /* more contacts than a lowered max_contacts (never with the default) */
+#define HUM_EFLAG_BAD_START_FRAME 8u    /* resetFromFrame start frame past the clip (the reference's iloc raises
+                                           IndexError): lane left unchanged */
 
 /* bookkeeping layout (doubles; integers stored exactly) */
 enum {
@@ -86,13 +88,30 @@ enum {
 /* hum_hier_step per-lane agent mask (which entries of the reference's obs/rew dicts are present) */
 #define HUM_AGENT_HIGH 1u   /* "high_level_agent" obs + reward */
 #define HUM_AGENT_LOW 2u    /* "low_level_agent" obs + reward */
+/* hum_hier_step `agent` selector values: 1 = high, 0 = low, HUM_AGENT_SEL_SKIP = the lane got no action this
+ * round (absent from RLlib's action dict): nothing is stepped or written for it except agents[i] = 0 */
+#define HUM_AGENT_SEL_SKIP 255u
 
 /* aux (RewardLogCallback, custom_callback.py:43-80) layout, float32 */
 enum {
     HUM_AUX_DELTA_JOINTS = 0, HUM_AUX_DELTA_END_POINTS, HUM_AUX_LOW_TARGET_SCORE, HUM_AUX_DELTA_VEL_JOINTS,
     HUM_AUX_BODY_POSTURE, HUM_AUX_HIGH_TARGET_SCORE, HUM_AUX_DRIFT_SCORE, HUM_AUX_BASE_REWARD, HUM_AUX_ALIVE,
-    HUM_AUX_ELECTRICITY, HUM_AUX_JOINT_LIMIT, HUM_AUX_DIST_FROM_ORIGIN
+    HUM_AUX_ELECTRICITY, HUM_AUX_JOINT_LIMIT, HUM_AUX_DIST_FROM_ORIGIN,
+    /* calcEndPointScore (low_level_env.py:361-382) of the lane's current state, frame, starting_ep_pos and
+       highLevelDegTarget, as the reference method returns it when called after step()/resetFromFrame()
+       (param_check.py:43-60): useExp=False and useExp=True.  Off the reward path in the reference (:445), so
+       HUM_AUX_DELTA_END_POINTS stays the reference attribute's constant 0. */
+    HUM_AUX_END_POINT_SCORE, HUM_AUX_END_POINT_SCORE_EXP,
+    HUM_AUX_ROBOT_POS /* 3: robot_pos (custom_callback.py:79 reads it) */
 };
+
+/* hum_config.numpy_semantics: the float32 scalar arithmetic of the reference under the NumPy it runs with.
+ * Two expressions mix a float32 numpy scalar with a Python float: `cur_obs[0] + initial_z` (calcAliveReward,
+ * low_level_env.py:386, hier_env.py:448) and `force_gain * power * self.power * np.clip(a[i], -1, 1)`
+ * (CustomHumanoidRobot.apply_action, humanoid.py:57-59).  NumPy 1.x (the reference's era: Ray 1.2.0, 2021)
+ * promotes them to float64; NumPy >= 2 (NEP 50) keeps float32. */
+#define HUM_NUMPY_1 1   /* default */
+#define HUM_NUMPY_2 2
 
 typedef struct hum_env hum_env;
 
@@ -123,6 +142,7 @@ typedef struct hum_config {
     int32_t lds_rows;         /* cooperative kernel: constraint rows per block kept in LDS; 0 (default) = the whole
                                  pool (envs_per_block * 30), k > 0 caps it at k rows so the rest take the global
                                  spill path (testing) */
+    int32_t numpy_semantics;  /* HUM_NUMPY_1 (default) or HUM_NUMPY_2, see above */
 } hum_config;
 
 /* Version / build info. */
@@ -151,7 +171,8 @@ int hum_set_lane_modes(hum_env* env, const uint32_t* modes);
 int hum_set_predefined_targets(hum_env* env, const double* xyz, int32_t n);
 
 /* reset()/resetFromFrame() (low_level_env.py:224-305) for lanes with lane_mask[i] != 0 (device u8, NULL = all).
- * start_frame (device i32, NULL = draw from the lane RNG as reset() does), reset_yaw_deg (device f64, NULL = 0).
+ * start_frame (device i32, NULL or < 0 = draw from the lane RNG as reset() does; >= the clip's pose rows =
+ * HUM_EFLAG_BAD_START_FRAME, lane unchanged), reset_yaw_deg (device f64, NULL = 0).
  * obs_out: device float32 [n,70] (rows of unmasked lanes untouched). */
 int hum_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
               float* obs_out, void* stream);
@@ -175,25 +196,8 @@ int hum_hier_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_
                    float* high_obs_out, void* stream);
 
 /* HierarchicalHumanoidEnv.step(action_dict) (hier_env.py:355-366, 538-641) for all lanes: each lane applies the
- * action of the agent it expects (the one that received an observation; `agent` (device u8 [n], 1 = high, 0 = low)
- * overrides it, NULL = expected): high_act [n,2] f32 -> high_level_step (no physics), low_act [n,17] f32 ->
- * low_level_step.  Outputs: agents [n] u8 (HUM_AGENT_* bits present in the reference's returned dicts),
- * high_obs [n,44] / low_obs [n,70] (rows written only where present), high_rew / low_rew [n] (0 where absent),
- * done [n] u8 (done["__all__"]), frame [n] i32 (may be NULL).  HUM_STEP_AUTORESET resets done lanes in the
- * same launch and writes their new high-level obs to high_obs_reset ([n,44], may be NULL). */
-int hum_hier_step(hum_env* env, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
-                  float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
-                  uint32_t flags, float* high_obs_reset, void* stream);
-
-/* HierarchicalHumanoidEnv.reset()/resetFromFrame() (hier_env.py:235-319) for masked lanes (hier handles only):
- * start_frame NULL = reset(): draw startFrame then resetYaw from the lane RNG (:239-240); given = resetFromFrame
- * with reset_yaw_deg (NULL = 0).  high_obs_out: device float32 [n,44] = {"high_level_agent": obs}. */
-int hum_hier_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
-                   float* high_obs_out, void* stream);
-
-/* HierarchicalHumanoidEnv.step(action_dict) (hier_env.py:355-366, 538-641) for all lanes: each lane applies the
- * action of the agent it expects (the one that received an observation; `agent` (device u8 [n], 1 = high, 0 = low)
- * overrides it, NULL = expected): high_act [n,2] f32 -> high_level_step (no physics), low_act [n,17] f32 ->
+ * action of the agent it expects (the one that received an observation; `agent` (device u8 [n], 1 = high, 0 = low,
+ * HUM_AGENT_SEL_SKIP = not stepped) overrides it, NULL = expected): high_act [n,2] f32 -> high_level_step (no physics), low_act [n,17] f32 ->
  * low_level_step.  Outputs: agents [n] u8 (HUM_AGENT_* bits present in the reference's returned dicts),
  * high_obs [n,44] / low_obs [n,70] (rows written only where present), high_rew / low_rew [n] (0 where absent),
  * done [n] u8 (done["__all__"]), frame [n] i32 (may be NULL).  HUM_STEP_AUTORESET resets done lanes in the

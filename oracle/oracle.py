@@ -136,13 +136,23 @@ def contacts(state, params=None):
     return out[:n]
 
 
-def motor_torques(action):
+# NumPy scalar-promotion semantics the reference runs under (include/humanoid_env.h, hum_config.numpy_semantics):
+# 1 = NumPy 1.x (the reference's era, Ray 1.2.0): float32 scalar (+|*) Python float -> float64; 2 = NumPy >= 2
+# (NEP 50, this image's 2.2 - the golden fixtures were made with it): the result stays float32.
+NUMPY_1, NUMPY_2 = 1, 2
+DEFAULT_NUMPY = NUMPY_1
+
+
+def motor_torques(action, numpy_semantics=DEFAULT_NUMPY):
     """humanoid.py:54-60: tau[dof] = float(1 * power * 0.41 * clip(a_i)) (action float32 as RLlib passes it)."""
     a = np.asarray(action)
     assert np.isfinite(a).all()
     tau = np.zeros(ND)
     for i in range(17):
-        tau[MOTOR_DOF[i]] = float(1 * MOTOR_POWER[i] * 0.41 * np.clip(a[i], -1, +1))
+        c = np.clip(a[i], -1, +1)
+        if numpy_semantics == NUMPY_1:
+            c = float(c)   # value-based promotion: the product is float64
+        tau[MOTOR_DOF[i]] = float(1 * MOTOR_POWER[i] * 0.41 * c)
     return tau
 
 
@@ -245,9 +255,10 @@ def get_joint_pos(clip, row, joint):
 class OracleLowLevelEnv:
     """Single-lane restatement of LowLevelHumanoidEnv (low_level_env.py:36-526)."""
 
-    def __init__(self, clip, seed=0, lane=0, params=None, rng=None):
+    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=DEFAULT_NUMPY):
         self.clip = clip
         self.params = params
+        self.numpy_semantics = numpy_semantics
         self.cur_timestep = 0
         self.max_timestep = 3000                                    # :73
         self.frame = 0
@@ -418,6 +429,8 @@ class OracleLowLevelEnv:
 
     def calcAliveReward(self):                                      # :384-387
         z = self.cur_obs[0] + 0.8
+        if self.numpy_semantics == NUMPY_1:
+            z = float(self.cur_obs[0]) + 0.8
         return +2 if z > 0.75 else -1
 
     def calcElectricityCost(self, action):                          # :389-394
@@ -482,7 +495,7 @@ class OracleLowLevelEnv:
     def step(self, action, debug=False, physics=True):              # :475-526
         action = np.asarray(action, dtype=np.float32)
         if physics:
-            self.state = phys_step(self.state, motor_torques(action), self.params)
+            self.state = phys_step(self.state, motor_torques(action, self.numpy_semantics), self.params)
         self.cur_obs = self._calc_state()
         self.robot_pos[0] = self.body_xyz[0]
         self.robot_pos[1] = self.body_xyz[1]

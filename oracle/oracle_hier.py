@@ -27,9 +27,10 @@ class OracleHierEnv:
     """Single-lane restatement of HierarchicalHumanoidEnv (hier_env.py:38-641).  `clip` is the selected motion
     (motion_list[selected_motion] = motion09_03, hier_env.py:50,179)."""
 
-    def __init__(self, clip, seed=0, lane=0, params=None, rng=None):
+    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=O.DEFAULT_NUMPY):
         self.clip = clip
         self.params = params
+        self.numpy_semantics = numpy_semantics
         self.step_per_level = 5                                     # :58
         self.steps_remaining_at_level = self.step_per_level
         self.num_high_level_steps = 0
@@ -207,6 +208,8 @@ class OracleHierEnv:
 
     def calcAliveReward(self):                                      # :446-449
         z = self.cur_obs[0] + 0.8
+        if self.numpy_semantics == O.NUMPY_1:
+            z = float(self.cur_obs[0]) + 0.8
         return +2 if z > 0.75 else -1
 
     def calcElectricityCost(self, action):                          # :451-456
@@ -289,7 +292,7 @@ class OracleHierEnv:
         action = np.asarray(action, dtype=np.float32)
         self.steps_remaining_at_level -= 1
         if physics:
-            self.state = O.phys_step(self.state, O.motor_torques(action), self.params)
+            self.state = O.phys_step(self.state, O.motor_torques(action, self.numpy_semantics), self.params)
         self.cur_obs = self._calc_state()
         self.updateReward(action=action)
         reward = [self.deltaJoints, self.deltaVelJoints, self.delta_lowTargetScore, self.electricityScore,

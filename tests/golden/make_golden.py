@@ -231,7 +231,7 @@ def run_scenario(name, clip, seed, lane, steps, act_seed, act_scale=1.0, reset_y
         env.cur_timestep += timestep_offset
     arng = np.random.default_rng(act_seed)
     out = {k: [] for k in ["action", "state_pre", "state_post", "torque", "obs", "reward", "done", "teleported",
-                           "cur_timestep_pre"]}
+                           "cur_timestep_pre", "endpoint_score", "endpoint_score_exp"]}
     books = []
     for t in range(steps):
         a = (arng.uniform(-1, 1, 17) * act_scale).astype(np.float32)
@@ -253,6 +253,10 @@ def run_scenario(name, clip, seed, lane, steps, act_seed, act_scale=1.0, reset_y
         out["reward"].append(float(r))
         out["done"].append(bool(done))
         out["teleported"].append(tele)
+        # calcEndPointScore (low_level_env.py:361-382) is off the reward path (:445): read it after the step the
+        # way param_check.py:43-60 does (a pure read of parts, frame, starting_ep_pos, highLevelDegTarget)
+        out["endpoint_score"].append(float(env.calcEndPointScore(useExp=False)))
+        out["endpoint_score_exp"].append(float(env.calcEndPointScore(useExp=True)))
         books.append(snapshot(env))
         if done:
             break
@@ -295,7 +299,7 @@ def main():
     for s in S:
         name = s.pop("name")
         allrec.update(run_scenario(name, **s))
-    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden_low.npz")
+    out = os.environ.get("GOLDEN_OUT", os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden_low.npz"))
     np.savez_compressed(out, **allrec)
     print("wrote", out, os.path.getsize(out), "bytes")
 

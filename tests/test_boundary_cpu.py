@@ -1,0 +1,75 @@
+"""CPU tests of the Python drop-in surface (no GPU, no Ray in this image): with stub `gym` / `ray.rllib`
+modules in place the env classes subclass the real framework bases (RLlib 1.2's BaseEnv.to_base_env only
+drives VectorEnv / BaseEnv subclasses directly, train_config.py:13-20,320-321), and registration creators give
+every env copy its own RNG stream (the reference's envs each own an unseeded default_rng, low_level_env.py:84)."""
+import importlib
+import sys
+import types
+
+import pytest
+
+
+class _EnvContext(dict):
+    """ray.rllib.env.env_context.EnvContext: a dict with worker_index / vector_index attributes."""
+
+    def __init__(self, d, worker_index, vector_index=0):
+        super().__init__(d)
+        self.worker_index, self.vector_index = worker_index, vector_index
+
+
+@pytest.fixture
+def stub_frameworks(monkeypatch):
+    class VectorEnv:
+        def __init__(self, observation_space, action_space, num_envs):
+            self.observation_space, self.action_space, self.num_envs = observation_space, action_space, num_envs
+
+    class BaseEnv:
+        pass
+
+    class Env:
+        pass
+
+    mods = {"ray": {}, "ray.rllib": {}, "ray.rllib.env": {}, "ray.rllib.env.vector_env": {"VectorEnv": VectorEnv},
+            "ray.rllib.env.base_env": {"BaseEnv": BaseEnv}, "gym": {"Env": Env}}
+    for name, attrs in mods.items():
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        monkeypatch.setitem(sys.modules, name, m)
+    import ilrl_amd.hier_env as H
+    import ilrl_amd.low_level_env as L
+    L2 = importlib.reload(L)
+    H2 = importlib.reload(H)
+    yield L2, H2, VectorEnv, BaseEnv, Env
+    monkeypatch.undo()
+    importlib.reload(L)
+    importlib.reload(H)
+
+
+def test_classes_subclass_framework_bases(stub_frameworks):
+    L, H, VectorEnv, BaseEnv, Env = stub_frameworks
+    assert issubclass(L.HumanoidVectorEnv, VectorEnv)
+    assert issubclass(H.HierarchicalVectorEnv, BaseEnv)
+    assert issubclass(L.LowLevelHumanoidEnv, Env)
+    for name in ("vector_reset", "reset_at", "vector_step", "get_unwrapped"):
+        assert callable(getattr(L.HumanoidVectorEnv, name))
+    for name in ("poll", "send_actions", "try_reset", "get_unwrapped"):
+        assert callable(getattr(H.HierarchicalVectorEnv, name))
+
+
+def test_without_frameworks_bases_are_object():
+    import ilrl_amd.low_level_env as L
+    if "ray" in sys.modules or "gym" in sys.modules:
+        pytest.skip("a real ray / gym is importable")
+    assert L.HumanoidVectorEnv.__mro__[1] is object
+
+
+def test_registration_seeds_are_distinct():
+    from ilrl_amd.low_level_env import env_seed
+    # no seed: OS entropy per env (the reference's unseeded default_rng)
+    assert env_seed(None)[0] != env_seed(None)[0]
+    # explicit seed: copies differ by their RLlib worker / vector index (global lane ranges never overlap)
+    offs = {env_seed(_EnvContext({"seed": 5}, w, v), 1024)[1] for w in range(7) for v in range(3)}
+    assert len(offs) == 21
+    assert {env_seed(_EnvContext({"seed": 5}, w, 0), 1024)[0] for w in range(7)} == {5}
+    lanes = sorted(env_seed(_EnvContext({"seed": 5}, w, 0), 1024)[1] for w in range(7))
+    assert all(b - a >= 1024 for a, b in zip(lanes, lanes[1:]))

@@ -1,0 +1,89 @@
+"""GPU tests of the C-ABI contract details (include/humanoid_env.h): lanes without an action are left
+untouched (hier send_actions), out-of-range resetFromFrame start frames are flagged without touching the lane,
+and captured step graphs see changed predefined courses / lane modes (they are re-captured)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from ilrl_amd import _native as N  # noqa: E402
+from ilrl_amd.hier_env import HierVecEnv  # noqa: E402
+from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+
+@pytest.mark.parametrize("kernel", [1, 0])
+def test_hier_skip_lanes_untouched(kernel):
+    n = 16
+    env = HierVecEnv(n, seed=2, kernel=kernel)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    # one high step everywhere, then low steps with every third lane absent from the action dict
+    env.step(torch.rand(n, 2, device="cuda", generator=g) * 2 - 1, None, agent=np.ones(n, np.uint8))
+    p0, b0 = env.get_state()
+    sel = np.zeros(n, np.uint8)
+    sel[::3] = N.HUM_AGENT_SEL_SKIP
+    agents, *_ = env.step(None, torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, agent=sel)
+    agents = agents.cpu().numpy()
+    p1, b1 = env.get_state()
+    skip = sel == N.HUM_AGENT_SEL_SKIP
+    assert (agents[skip] == 0).all() and (agents[~skip] != 0).all()
+    np.testing.assert_array_equal(p1[skip], p0[skip])
+    np.testing.assert_array_equal(b1[skip], b0[skip])
+    assert (np.abs(p1[~skip] - p0[~skip]).max(axis=1) > 0).all()
+    env.close()
+
+
+def test_start_frame_out_of_range_flagged():
+    env = HumanoidVecEnv(4, clips=("motion09_03",), seed=1)
+    env.reset()
+    p0, b0 = env.get_state()
+    npos = env.clips[0].pos.shape[0]
+    sf = torch.tensor([5, npos, npos + 100, 7], dtype=torch.int32, device="cuda")
+    env.reset(start_frame=sf)
+    p1, b1 = env.get_state()
+    assert env.error_flags() & N.HUM_EFLAG_BAD_START_FRAME
+    np.testing.assert_array_equal(p1[1:3], p0[1:3])
+    np.testing.assert_array_equal(b1[1:3], b0[1:3])
+    assert b1[0, N.BK["frame"]] == 7 and b1[3, N.BK["frame"]] == 9   # resetFromFrame + incFrame(2)
+    env.close()
+
+
+def _graph_step(env, a, k):
+    rc = N.lib().hum_step_graph(env.h, N.ctypes.c_void_p(a.data_ptr()), N.ctypes.c_void_p(env.obs.data_ptr()),
+                                N.ctypes.c_void_p(env.reward.data_ptr()), N.ctypes.c_void_p(env.done.data_ptr()),
+                                N.ctypes.c_void_p(env.frame.data_ptr()), N.HUM_STEP_AUTORESET,
+                                N.ctypes.c_void_p(env.obs_reset.data_ptr()), k)
+    assert rc == 0
+
+
+def test_graph_recaptured_after_predefined_targets_change():
+    """step_graph, then set_predefined_targets (frees and reallocates the course), then step_graph again: the
+    graph must not replay the freed course; results equal the eager path."""
+    n = 64
+    envs = [HumanoidVecEnv(n, clips=("motion08_03",), seed=9) for _ in range(2)]
+    course1 = np.array([[0.3, 0.0, 0.0], [0.6, 0.1, 0.0]])
+    course2 = np.array([[0.2, 0.2, 0.0], [0.4, -0.3, 0.0], [0.1, 0.1, 0.0]])
+    for e in envs:
+        e.set_predefined_targets(course1)
+        e.set_modes(predefined=True)
+        e.reset()
+    a = (torch.rand(n, 17, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) * 0.3).contiguous()
+    for step in range(2):
+        if step == 1:
+            for e in envs:
+                e.set_predefined_targets(course2)
+        for _ in range(6):
+            envs[0].step(a, autoreset=True)
+        torch.cuda.synchronize()
+        _graph_step(envs[1], a, 6)
+        envs[1].sync()
+        p0, b0 = envs[0].get_state()
+        p1, b1 = envs[1].get_state()
+        np.testing.assert_array_equal(p0, p1)
+        np.testing.assert_array_equal(b0, b1)
+    for e in envs:
+        e.close()

@@ -66,7 +66,7 @@ def book_rows(r):
 
 def run_scenario(r, precision, skip_physics, kernel=1):
     T = len(r["done"])
-    env = HierVecEnv(T, precision=precision, kernel=kernel)
+    env = HierVecEnv(T, precision=precision, kernel=kernel, numpy_semantics=N.HUM_NUMPY_2)   # fixtures: numpy 2.2
     if len(r["predefined"]):
         env.set_predefined_targets(r["predefined"])
     phys = r["state_post"] if skip_physics else r["state_pre"]

@@ -11,14 +11,14 @@ from ilrl_amd.clips import load_clip
 
 def replay_oracle(r):
     clip = load_clip(str(r["clip"]))
-    env = O.OracleLowLevelEnv(clip, rng=ScriptedRNG(r["draws"]))
+    env = O.OracleLowLevelEnv(clip, rng=ScriptedRNG(r["draws"]), numpy_semantics=O.NUMPY_2)   # fixtures: numpy 2.2
     seed, lane, act_seed, debug, reset_yaw, start_frame, ts_off = [int(x) for x in r["meta"]]
     if len(r["predefined"]):
         env.usePredefinedTarget = True
         env.predefinedTarget = r["predefined"].copy()
     obs0 = env.reset(resetYaw=reset_yaw) if start_frame < 0 else env.resetFromFrame(start_frame, resetYaw=reset_yaw)
     out = {"obs0": obs0, "state0": env.state.copy(), "obs": [], "reward": [], "done": [], "state_post": [],
-           "book": []}
+           "book": [], "endpoint": [], "endpoint_exp": []}
     for t in range(len(r["reward"])):
         env.state = r["state_pre"][t].copy()          # identical physics input (teleports included)
         env.cur_timestep = int(r["cur_timestep_pre"][t])
@@ -27,6 +27,8 @@ def replay_oracle(r):
         out["reward"].append(rew)
         out["done"].append(done)
         out["state_post"].append(env.state.copy())
+        out["endpoint"].append(env.calcEndPointScore(useExp=False))
+        out["endpoint_exp"].append(env.calcEndPointScore(useExp=True))
         b = {k: getattr(env, k) for k in BOOK_SCALARS}
         b.update({k: np.array(getattr(env, k), dtype=np.float64) for k in BOOK_VECS if k != "walk_target"})
         b["walk_target"] = np.array(env.walk_target)
@@ -53,6 +55,35 @@ def test_oracle_matches_reference(golden, name):
     np.testing.assert_array_equal(np.array(o["obs"]), r["obs"])
     np.testing.assert_array_equal(np.array(o["reward"]), r["reward"])
     np.testing.assert_array_equal(np.array(o["done"]), r["done"])
+    # calcEndPointScore (R12, off the reward path) read after each step
+    np.testing.assert_array_equal(np.array(o["endpoint"]), r["endpoint_score"])
+    np.testing.assert_array_equal(np.array(o["endpoint_exp"]), r["endpoint_score_exp"])
     for k in BOOK_SCALARS + BOOK_VECS:
         got = np.array([b[k] for b in o["book"]], dtype=np.float64)
         np.testing.assert_array_equal(got, r["book_" + k].astype(np.float64), err_msg=k)
+
+
+def test_numpy_semantics_fixture():
+    """The two float32-scalar expressions (calcAliveReward, apply_action) against the reference's own methods
+    run under NumPy 2.2 (tests/golden/make_golden_numpy.py): the oracle's HUM_NUMPY_2 mode is exact; its
+    HUM_NUMPY_1 mode (float64 promotion, restated - no NumPy 1.x here) differs exactly at the boundary."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_numpy.npz"), allow_pickle=False)
+    clip = load_clip("motion02_04")
+    alive1 = []
+    for x, want in zip(g["obs0"], g["alive"]):
+        for sem, out in ((O.NUMPY_2, None), (O.NUMPY_1, alive1)):
+            env = O.OracleLowLevelEnv(clip, numpy_semantics=sem)
+            env.cur_obs = np.zeros(42, np.float32)
+            env.cur_obs[0] = x
+            got = env.calcAliveReward()
+            if out is None:
+                assert got == want, (x, got, want)
+            else:
+                out.append(got)
+                assert got == (2 if float(x) + 0.8 > 0.75 else -1)
+    assert (np.array(alive1) != g["alive"]).sum() >= 3   # float32 neighbours of -0.05 decide differently
+    for a, tq in zip(g["action"], g["torque"]):
+        np.testing.assert_array_equal(O.motor_torques(a, O.NUMPY_2), tq)
+        t1 = O.motor_torques(a, O.NUMPY_1)
+        np.testing.assert_allclose(t1, tq, rtol=1e-7, atol=0)   # float64 vs float32 product

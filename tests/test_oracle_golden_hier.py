@@ -4,6 +4,7 @@ tests/golden/make_golden_hier.py)."""
 import numpy as np
 import pytest
 
+import oracle as O
 import oracle_hier as OH
 from golden_replay import ScriptedRNG, rec
 from ilrl_amd.clips import load_clip
@@ -18,7 +19,7 @@ HIER_VEC = ["target", "starting_robot_pos", "robot_pos", "starting_ep_pos"]
 
 
 def replay_oracle_hier(r):
-    env = OH.OracleHierEnv(load_clip("motion09_03"), rng=ScriptedRNG(r["draws"]))
+    env = OH.OracleHierEnv(load_clip("motion09_03"), rng=ScriptedRNG(r["draws"]), numpy_semantics=O.NUMPY_2)
     seed, lane, act_seed, debug, reset_yaw, start_frame, ts_off = [int(x) for x in r["meta"]]
     if len(r["predefined"]):
         env.usePredefinedTarget = True
