@@ -307,6 +307,27 @@ class OracleLowLevelEnv:
         self.delta_bodyPostureScore = 0
         self.delta_highTargetScore = 0
 
+    @classmethod
+    def from_lane(cls, clip, phys, book, bk, numpy_semantics=DEFAULT_NUMPY):
+        """An env holding exactly one product lane's state: phys [47] and book [HUM_NBOOK] as hum_get_state
+        returns them, bk = the HUM_BK_* column map (ilrl_amd._native.BK, passed in: the oracle imports nothing
+        from the product).  Its RNG continues the lane's stream (key words + counter)."""
+        o = cls(clip, numpy_semantics=numpy_semantics)
+        o.state = np.array(phys, dtype=np.float64).copy()
+        o.frame = int(book[bk["frame"]])
+        o.cur_timestep = int(book[bk["cur_timestep"]])
+        o.predefinedTargetIndex = int(book[bk["predefinedTargetIndex"]])
+        for k in ("target", "starting_robot_pos", "robot_pos", "starting_ep_pos"):
+            setattr(o, k, np.array(book[bk[k]:bk[k] + 3], dtype=np.float64))
+        o.walk_target = (float(book[bk["walk_target"]]), float(book[bk["walk_target"] + 1]))
+        o.highLevelDegTarget = float(book[bk["highLevelDegTarget"]])
+        for k in ("lowTargetScore", "deltaJoints", "deltaVelJoints", "bodyPostureScore", "electricityScore",
+                  "jointLimitScore", "aliveReward", "delta_lowTargetScore"):
+            setattr(o, k, float(book[bk[k]]))
+        key = int(book[bk["rng_key_lo"]]) | (int(book[bk["rng_key_hi"]]) << 32)
+        o.rng = LaneRNG(key=key, counter=int(book[bk["rng_counter"]]))
+        return o
+
     # -- physics-facing helpers (stand in for flat_env / robot) ----------------------------------------
     def _calc_state(self):
         obs, body_xyz, js, jal, rpy = calc_state(self.state, self.walk_target)

@@ -10,23 +10,8 @@ BK = N.BK
 
 
 def oracle_from_lane(clip, phys, book):
-    """OracleLowLevelEnv whose physics state and bookkeeping are one lane's hum_get_state rows (phys [47],
-    book [HUM_NBOOK]); its RNG continues the lane's stream (key words + counter)."""
-    o = O.OracleLowLevelEnv(clip)
-    o.state = np.array(phys, dtype=np.float64).copy()
-    o.frame = int(book[BK["frame"]])
-    o.cur_timestep = int(book[BK["cur_timestep"]])
-    o.predefinedTargetIndex = int(book[BK["predefinedTargetIndex"]])
-    for k in ("target", "starting_robot_pos", "robot_pos", "starting_ep_pos"):
-        setattr(o, k, np.array(book[BK[k]:BK[k] + 3], dtype=np.float64))
-    o.walk_target = (float(book[BK["walk_target"]]), float(book[BK["walk_target"] + 1]))
-    o.highLevelDegTarget = float(book[BK["highLevelDegTarget"]])
-    for k in ("lowTargetScore", "deltaJoints", "deltaVelJoints", "bodyPostureScore", "electricityScore",
-              "jointLimitScore", "aliveReward", "delta_lowTargetScore"):
-        setattr(o, k, float(book[BK[k]]))
-    key = int(book[BK["rng_key_lo"]]) | (int(book[BK["rng_key_hi"]]) << 32)
-    o.rng = O.LaneRNG(key=key, counter=int(book[BK["rng_counter"]]))
-    return o
+    """OracleLowLevelEnv whose physics state, bookkeeping and RNG stream are one lane's hum_get_state rows."""
+    return O.OracleLowLevelEnv.from_lane(clip, phys, book, BK)
 
 
 def contact_heavy_states(n, min_contacts=17, seed=1):

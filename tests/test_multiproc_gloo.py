@@ -30,7 +30,10 @@ def _worker(rank, world, port, n_total, q):
     rew = torch.full((n,), float(rank))
     done = torch.zeros(n, dtype=torch.uint8)
     done[0] = 1
-    g = gather_trajectories([obs, rew, done, draws], dst=0)
+    big = (torch.arange(off, off + n, dtype=torch.int64) + (1 << 40)).reshape(n, 1).repeat(1, 2)   # > 2**24
+    frame = torch.arange(off, off + n, dtype=torch.int32) * 16777217
+    f64 = torch.arange(off, off + n, dtype=torch.float64) / 3.0
+    g = gather_trajectories([obs, rew, done, draws, big, frame, f64], dst=0)
     if rank == 0:
         q.put([t.numpy() for t in g])
     dist.barrier()
@@ -48,21 +51,27 @@ def test_shard_covers_all_lanes():
 
 
 @pytest.mark.timeout(120)
-def test_gloo_world2_gather_and_rng_independent_of_sharding():
+@pytest.mark.parametrize("n_total", [10, 7])   # 7 lanes over 2 ranks: uneven shards (4 + 3)
+def test_gloo_world2_gather_and_rng_independent_of_sharding(n_total):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    n_total = 10
     procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
     for p in procs:
         p.start()
-    obs, rew, done, draws = q.get(timeout=100)
+    obs, rew, done, draws, big, frame, f64 = q.get(timeout=100)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    n0 = shard(n_total, 2, 0)[1]
     assert obs.shape == (n_total, 70)
     np.testing.assert_array_equal(obs.reshape(-1), np.arange(n_total * 70, dtype=np.float32))
-    np.testing.assert_array_equal(rew, [0] * 5 + [1] * 5)
-    np.testing.assert_array_equal(done, [1, 0, 0, 0, 0, 1, 0, 0, 0, 0])
+    np.testing.assert_array_equal(rew, [0] * n0 + [1] * (n_total - n0))
+    np.testing.assert_array_equal(done, [1] + [0] * (n0 - 1) + [1] + [0] * (n_total - n0 - 1))
+    # lossless for every dtype (the round-1 gather cast through float32)
+    assert big.dtype == np.int64 and frame.dtype == np.int32 and f64.dtype == np.float64
+    np.testing.assert_array_equal(big[:, 0], np.arange(n_total, dtype=np.int64) + (1 << 40))
+    np.testing.assert_array_equal(frame, (np.arange(n_total) * 16777217).astype(np.int32))
+    np.testing.assert_array_equal(f64, np.arange(n_total, dtype=np.float64) / 3.0)
     single = np.array([[O.lane_draw(5, i, c, 0, 293) for c in range(3)] for i in range(n_total)], dtype=np.float32)
     np.testing.assert_array_equal(draws, single)
