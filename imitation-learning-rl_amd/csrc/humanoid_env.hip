@@ -285,7 +285,13 @@ int hum_set_predefined_targets(hum_env* e, const double* xyz, int32_t n) {
 
 int hum_reset(hum_env* e, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
               float* obs_out, void* stream) {
+    return hum_reset_ex(e, lane_mask, start_frame, reset_yaw_deg, 0u, obs_out, stream);
+}
+
+int hum_reset_ex(hum_env* e, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+                 uint32_t flags, float* obs_out, void* stream) {
     if (!e) return fail(HUM_ERR_ARG, "hum_reset: null env");
+    if (flags & ~(HUM_RESET_NO_REF_POSE | HUM_RESET_NO_INIT_VEL)) return fail(HUM_ERR_ARG, "hum_reset: unknown flags");
     if (e->cfg.hier) return fail(HUM_ERR_STATE, "hum_reset: hierarchical handle (use hum_hier_reset)");
     if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_reset: no clip uploaded (hum_set_clip)");
     HIPCHK(hipSetDevice(e->cfg.device));
@@ -293,6 +299,7 @@ int hum_reset(hum_env* e, const uint8_t* lane_mask, const int32_t* start_frame, 
     a.mask = lane_mask;
     a.start_frame = start_frame;
     a.reset_yaw = reset_yaw_deg;
+    a.reset_flags = flags;
     a.obs = obs_out;
     hipStream_t s = stream_of(e, stream);
     if (e->cfg.precision) hipLaunchKernelGGL(reset_kernel<double>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);
@@ -320,7 +327,13 @@ int hum_step(hum_env* e, const float* actions, float* obs, float* reward, uint8_
 
 int hum_hier_reset(hum_env* e, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
                    float* high_obs_out, void* stream) {
+    return hum_hier_reset_ex(e, lane_mask, start_frame, reset_yaw_deg, 0u, high_obs_out, stream);
+}
+
+int hum_hier_reset_ex(hum_env* e, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+                      uint32_t flags, float* high_obs_out, void* stream) {
     if (!e) return fail(HUM_ERR_ARG, "hum_hier_reset: null env");
+    if (flags & ~(HUM_RESET_NO_REF_POSE | HUM_RESET_NO_INIT_VEL)) return fail(HUM_ERR_ARG, "hum_hier_reset: unknown flags");
     if (!e->cfg.hier) return fail(HUM_ERR_STATE, "hum_hier_reset: handle was not created with hier = 1");
     if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_hier_reset: no clip uploaded (hum_set_clip)");
     HIPCHK(hipSetDevice(e->cfg.device));
@@ -328,6 +341,7 @@ int hum_hier_reset(hum_env* e, const uint8_t* lane_mask, const int32_t* start_fr
     a.mask = lane_mask;
     a.start_frame = start_frame;
     a.reset_yaw = reset_yaw_deg;
+    a.reset_flags = flags;
     a.obs_high = high_obs_out;
     hipStream_t s = stream_of(e, stream);
     if (e->cfg.precision) hipLaunchKernelGGL(reset_kernel<double>, grid_of(e), dim3(e->cfg.block_size), 0, s, a);

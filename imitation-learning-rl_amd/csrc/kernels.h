@@ -54,6 +54,7 @@ struct KArgs {
     const unsigned char* mask;
     const int* start_frame;
     const double* reset_yaw;
+    unsigned reset_flags;           // HUM_RESET_* (resetFromFrame startFromRef / initVel = False)
     float* aux;
     // hierarchical env (hum_hier_step / hum_hier_reset)
     int hier;
@@ -128,17 +129,36 @@ __device__ inline int draw(const KArgs& a, int i, Book& b, int lo, int hi) {
     return lane_draw_key(b.rng_key, b.rng_ctr++, lo, hi);
 }
 
+// flat_env.reset()'s WalkerBase.robot_specific_reset: every joint at U(-0.1, 0.1), velocity 0, drawn from the
+// robot's own np_random (a stream apart from the env's rng): key' = splitmix64(key ^ salt), 32 counters per
+// reset taken at the env stream's current counter (oracle/oracle.py::LaneRNG.joint_noise)
+template <typename T>
+__device__ inline void joint_noise(const Book& b, T* st) {
+    const unsigned long long k2 = splitmix64(b.rng_key ^ 0xD1B54A32D192ED03ull);
+#pragma unroll
+    for (int d = 0; d < NDOF; d++) {
+        const unsigned long long x = splitmix64(k2 + (((unsigned long long)b.rng_ctr << 5) | (unsigned)d));
+        const double u = (double)(x >> 11) * 0x1.0p-53;
+        st[13 + d] = (T)(-0.1 + (0.1 - -0.1) * u);
+        st[30 + d] = T(0);
+    }
+}
+
 // ----------------------------------------------------------------------------------- reset
 // LowLevelHumanoidEnv.reset() / resetFromFrame() (low_level_env.py:224-305)
 template <typename T>
 __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* obs,
                            unsigned& ef, const T* scs = nullptr) {   // scs: the reset pose's hinge sin / cos
     const ClipDev& c = a.clips[b.clip];
-    if (start_frame < 0) start_frame = draw(a, i, b, 0, c.max_frame - 5);   // :228
-    // flat_env.reset(): restoreState -> zero velocities (all 17 joints overwritten below)
+    const bool ref = !(a.reset_flags & HUM_RESET_NO_REF_POSE);                // startFromRef
+    const bool init_vel = ref && !(a.reset_flags & HUM_RESET_NO_INIT_VEL);   // startFromRef and initVel (:291)
+    if (ref && start_frame < 0) start_frame = draw(a, i, b, 0, c.max_frame - 5);   // :228
+    // flat_env.reset(): restoreState -> zero velocities, joints re-randomised (all 17 overwritten below when
+    // starting from the reference)
 #pragma unroll
     for (int e = 0; e < HUM_NSTATE; e++) st[e] = 0;
     st[6] = 1;
+    if (!ref) joint_noise(b, st);
     b.timestep = 0;
     if ((b.mode & HUM_MODE_PREDEFINED) && a.npred > 0) {                   // :253-255
         b.pred_idx = 0;
@@ -149,13 +169,15 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
         b.target[1] = sin(r) * 5;
         b.target[2] = 0;
     }
-    b.frame = start_frame;                                                  // :259-261 setJointsOrientation
-    int vrow = start_frame;
-    if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
+    if (ref) {                                                              // :259-261 setJointsOrientation
+        b.frame = start_frame;
+        int vrow = start_frame;
+        if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
 #pragma unroll
-    for (int j = 0; j < NREF; j++) {
-        st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
-        st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+        for (int j = 0; j < NREF; j++) {
+            st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
+            st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+        }
     }
     for (int k = 0; k < 3; k++) { b.robot_pos[k] = 0; b.srp[k] = 0; }      // :264-268
     st[0] = 0; st[1] = 0; st[2] = (T)1.17;
@@ -172,7 +194,7 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
     const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
     {
         Kin<T> K;
-        if (scs) forward_kinematics_pre(st + 3, scs, K);
+        if (scs && ref) forward_kinematics_pre(st + 3, scs, K);
         else forward_kinematics(st + 3, st + 13, K);
         T pp[NPART][3];
         part_positions(K, pp);
@@ -185,16 +207,18 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
         b.sep[0] = rfx - refx; b.sep[1] = rfy - refy; b.sep[2] = 0;
         const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
         const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
-        st[7] = (T)(((l1x - l0x) / 0.0165) / 1.2);
-        st[8] = (T)(((l1y - l0y) / 0.0165) / 1.2);
-        st[9] = (T)(((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165) / 1.2);
+        if (init_vel) {
+            st[7] = (T)(((l1x - l0x) / 0.0165) / 1.2);
+            st[8] = (T)(((l1y - l0y) / 0.0165) / 1.2);
+            st[9] = (T)(((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165) / 1.2);
+        }
     }
     b.lts = 0; b.dj = 0; b.dvj = 0; b.bps = 0; b.es = 0; b.jls = 0; b.alive = 0; b.dlts = 0;   // initReward
     inc_frame(b, c, 2);                                                     // :302
     float js[NDOF];
     int jal;
     PostPhys<T> pp;
-    calc_state(st, b.wt, obs, js, jal, pp, scs);                            // :304-305
+    calc_state(st, b.wt, obs, js, jal, pp, ref ? scs : nullptr);            // :304-305
     ref_obs(c, b.frame, obs + 42, ef);
 }
 
@@ -319,6 +343,8 @@ template <typename T>
 __device__ void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* o44,
                                 unsigned& ef) {
     const ClipDev& c = a.clips[b.clip];
+    const bool ref = !(a.reset_flags & HUM_RESET_NO_REF_POSE);
+    const bool init_vel = ref && !(a.reset_flags & HUM_RESET_NO_INIT_VEL);
     if (start_frame < 0) {                                                  // :238-241 (argument order)
         start_frame = draw(a, i, b, 0, c.max_frame - 5);
         reset_yaw = (double)draw(a, i, b, -180, 180);
@@ -326,6 +352,7 @@ __device__ void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start
 #pragma unroll
     for (int e = 0; e < HUM_NSTATE; e++) st[e] = 0;                         // flat_env.reset()
     st[6] = 1;
+    if (!ref) joint_noise(b, st);
     b.timestep = 0;
     if ((b.mode & HUM_MODE_PREDEFINED) && a.npred > 0) {                   // :264-266
         b.pred_idx = 0;
@@ -336,13 +363,15 @@ __device__ void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start
         b.target[1] = sin(r) * 5;
         b.target[2] = 0;
     }
-    b.frame = start_frame;                                                  // :272-274 setJointsOrientation
-    int vrow = start_frame;
-    if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
+    if (ref) {                                                              // :272-274 setJointsOrientation
+        b.frame = start_frame;
+        int vrow = start_frame;
+        if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
 #pragma unroll
-    for (int j = 0; j < NREF; j++) {
-        st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
-        st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+        for (int j = 0; j < NREF; j++) {
+            st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
+            st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+        }
     }
     for (int k = 0; k < 3; k++) { b.robot_pos[k] = 0; b.srp[k] = 0; }      // :277-281
     st[0] = 0; st[1] = 0; st[2] = (T)1.17;
@@ -360,9 +389,11 @@ __device__ void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start
         const double* e1 = c.ep + f1 * 27;
         const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
         const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
-        st[7] = (T)((l1x - l0x) / 0.0165);
-        st[8] = (T)((l1y - l0y) / 0.0165);
-        st[9] = (T)((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165);
+        if (init_vel) {
+            st[7] = (T)((l1x - l0x) / 0.0165);
+            st[8] = (T)((l1y - l0y) / 0.0165);
+            st[9] = (T)((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165);
+        }
     }
     // initReward (:183-206); starting_ep_pos is NOT reset by the hierarchical env
     b.lts = 0; b.dj = 0; b.dvj = 0; b.bps = 0; b.es = 0; b.jls = 0; b.alive = 0; b.dlts = 0;
@@ -757,7 +788,7 @@ __global__ void __launch_bounds__(256) reset_kernel(KArgs a) {
     {   // resetFromFrame past the clip: the reference's DataFrame.iloc raises IndexError (low_level_env.py:208,
         // :282-291; hier_env.py:293-304 also reads end-point row startFrame + 1)
         const ClipDev& c = a.clips[b.clip];
-        if (sf >= (a.hier ? c.n_pos - 1 : c.n_pos)) {
+        if (!(a.reset_flags & HUM_RESET_NO_REF_POSE) && sf >= (a.hier ? c.n_pos - 1 : c.n_pos)) {
             atomicOr(a.eflags, HUM_EFLAG_BAD_START_FRAME);
             return;
         }

@@ -16,6 +16,7 @@ HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS = 1, 2
 HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
 HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW, HUM_EFLAG_BAD_START_FRAME = 1, 2, 4, 8
 HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
+HUM_RESET_NO_REF_POSE, HUM_RESET_NO_INIT_VEL = 1, 2
 HUM_MAX_CONTACTS = 95
 
 # bookkeeping layout (HUM_BK_*)
@@ -34,7 +35,8 @@ AUX = ["deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bod
 EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_create", "hum_destroy", "hum_set_clip",
            "hum_set_lane_clips", "hum_set_lane_modes", "hum_set_predefined_targets", "hum_reset", "hum_step",
            "hum_step_graph", "hum_get_aux", "hum_get_state", "hum_set_state", "hum_get_parts",
-           "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step"]
+           "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step",
+           "hum_reset_ex", "hum_hier_reset_ex"]
 
 
 class HumConfig(ctypes.Structure):
@@ -80,6 +82,8 @@ def lib():
     L.hum_set_lane_modes.argtypes = [vp, vp]
     L.hum_set_predefined_targets.argtypes = [vp, dp, i32]
     L.hum_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.hum_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+    L.hum_hier_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.hum_step.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, vp]
     L.hum_hier_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hum_hier_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp]

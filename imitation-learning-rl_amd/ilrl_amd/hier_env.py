@@ -45,14 +45,11 @@ class HierVecEnv(HumanoidVecEnv):
         self._zero_high = t.zeros(self.n, N.HUM_NACT_HIGH, dtype=f32, device=self.device)
         self._zero_low = t.zeros(self.n, N.HUM_NACT, dtype=f32, device=self.device)
 
-    def reset(self, mask=None, start_frame=None, reset_yaw=None):
+    def reset(self, mask=None, start_frame=None, reset_yaw=None, start_from_ref=True, init_vel=True):
         """reset() (start_frame None: startFrame and resetYaw drawn per lane) or resetFromFrame(); -> [n,44]."""
-        t = self.torch
-        m = None if mask is None else t.as_tensor(mask, dtype=t.uint8, device=self.device).contiguous()
-        sf = None if start_frame is None else t.as_tensor(start_frame, dtype=t.int32, device=self.device).expand(self.n).contiguous()
-        ry = None if reset_yaw is None else t.as_tensor(reset_yaw, dtype=t.float64, device=self.device).expand(self.n).contiguous()
-        N.check(N.lib().hum_hier_reset(self.h, _ptr(m), _ptr(sf), _ptr(ry), _ptr(self.obs_high), self._stream()),
-                "hum_hier_reset")
+        m, sf, ry, flags = self._reset_args(mask, start_frame, reset_yaw, start_from_ref, init_vel)
+        N.check(N.lib().hum_hier_reset_ex(self.h, _ptr(m), _ptr(sf), _ptr(ry), flags, _ptr(self.obs_high),
+                                          self._stream()), "hum_hier_reset")
         return self.obs_high
 
     def _act(self, a, width, zero):
@@ -147,10 +144,11 @@ class HierarchicalHumanoidEnv(_HierBookView):
         return {HIGH: self._v.reset()[0].double().cpu().numpy()}
 
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :259-319
-        if not (startFromRef and initVel):
-            raise NotImplementedError("resetFromFrame supports startFromRef=True, initVel=True (all reference callers)")
+        if startFromRef and not 0 <= int(startFrame) < self._v.clips[0].pos.shape[0] - 1:   # iloc (:293-304)
+            raise IndexError("single positional indexer is out-of-bounds (startFrame=%d)" % int(startFrame))
         self.__dict__["_cache"] = None
-        return {HIGH: self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw))[0].double().cpu().numpy()}
+        return {HIGH: self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw), start_from_ref=startFromRef,
+                                    init_vel=initVel)[0].double().cpu().numpy()}
 
     def step(self, action_dict, debug=False):                           # :355-366
         assert len(action_dict) == 1, action_dict

@@ -153,11 +153,10 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
         return self._obs(self._v.reset(reset_yaw=float(resetYaw)))
 
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :247-305
-        if not (startFromRef and initVel):
-            raise NotImplementedError("resetFromFrame supports startFromRef=True, initVel=True (all reference callers)")
-        if not 0 <= int(startFrame) < self.max_frame + 1:   # DataFrame.iloc (:208) raises past the table
+        if startFromRef and not 0 <= int(startFrame) < self.max_frame + 1:   # DataFrame.iloc (:208) raises
             raise IndexError("single positional indexer is out-of-bounds (startFrame=%d)" % int(startFrame))
-        return self._obs(self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw)))
+        return self._obs(self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw),
+                                       start_from_ref=startFromRef, init_vel=initVel))
 
     def step(self, action, debug=False):                                # :322-323, :475-526
         a = np.asarray(action, dtype=np.float32).reshape(1, 17)

@@ -83,13 +83,20 @@ class HumanoidVecEnv:
         xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
         N.check(N.lib().hum_set_predefined_targets(self.h, _dp(xyz), xyz.shape[0]), "hum_set_predefined_targets")
 
-    def reset(self, mask=None, start_frame=None, reset_yaw=None):
-        """reset()/resetFromFrame() for masked lanes; returns the obs tensor [n,70] (device)."""
+    def _reset_args(self, mask, start_frame, reset_yaw, start_from_ref, init_vel):
         t = self.torch
         m = None if mask is None else t.as_tensor(mask, dtype=t.uint8, device=self.device).contiguous()
         sf = None if start_frame is None else t.as_tensor(start_frame, dtype=t.int32, device=self.device).expand(self.n).contiguous()
         ry = None if reset_yaw is None else t.as_tensor(reset_yaw, dtype=t.float64, device=self.device).expand(self.n).contiguous()
-        N.check(N.lib().hum_reset(self.h, _ptr(m), _ptr(sf), _ptr(ry), _ptr(self.obs), self._stream()), "hum_reset")
+        flags = (0 if start_from_ref else N.HUM_RESET_NO_REF_POSE) | (0 if init_vel else N.HUM_RESET_NO_INIT_VEL)
+        return m, sf, ry, flags
+
+    def reset(self, mask=None, start_frame=None, reset_yaw=None, start_from_ref=True, init_vel=True):
+        """reset()/resetFromFrame(startFrame, resetYaw, startFromRef, initVel) for masked lanes; returns the obs
+        tensor [n,70] (device)."""
+        m, sf, ry, flags = self._reset_args(mask, start_frame, reset_yaw, start_from_ref, init_vel)
+        N.check(N.lib().hum_reset_ex(self.h, _ptr(m), _ptr(sf), _ptr(ry), flags, _ptr(self.obs), self._stream()),
+                "hum_reset")
         return self.obs
 
     def step(self, actions, autoreset=False, skip_physics=False):

@@ -56,6 +56,11 @@ extern "C" {
 #define HUM_STEP_AUTORESET 1u     /* reset done lanes inside the same launch (obs_reset receives the new obs) */
 #define HUM_STEP_SKIP_PHYSICS 2u  /* treat the current physics state as post-step (parity: injected physics) */
 
+/* hum_reset_ex / hum_hier_reset_ex flags: resetFromFrame(startFromRef, initVel) (low_level_env.py:247-305,
+ * hier_env.py:259-319); both False-able independently, default (0) = True, True as reset() uses */
+#define HUM_RESET_NO_REF_POSE 1u  /* startFromRef=False: frame unchanged, joints at flat_env.reset()'s U(-0.1, 0.1) */
+#define HUM_RESET_NO_INIT_VEL 2u  /* initVel=False: no starting base velocity from the reference */
+
 /* per-lane mode bits (hum_set_lane_modes) */
 #define HUM_MODE_DEBUG 1u         /* step(action, debug=True): done only on fall (low_level_env.py:470-471) */
 #define HUM_MODE_PREDEFINED 2u    /* usePredefinedTarget (low_level_env.py:253-255, 419-421) */
@@ -177,6 +182,10 @@ int hum_set_predefined_targets(hum_env* env, const double* xyz, int32_t n);
 int hum_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
               float* obs_out, void* stream);
 
+/* hum_reset with resetFromFrame's startFromRef / initVel switches (HUM_RESET_* flags). */
+int hum_reset_ex(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+                 uint32_t flags, float* obs_out, void* stream);
+
 /* step(action) (low_level_env.py:475-526) for all lanes: device float32 actions [n,17] ->
  * obs [n,70] f32, reward [n] f32, done [n] u8, frame [n] i32 (frame may be NULL).
  * With HUM_STEP_AUTORESET, done lanes are reset in the same launch; their post-reset observation is
@@ -194,6 +203,10 @@ int hum_step_graph(hum_env* env, const float* actions, float* obs, float* reward
  * with reset_yaw_deg (NULL = 0).  high_obs_out: device float32 [n,44] = {"high_level_agent": obs}. */
 int hum_hier_reset(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
                    float* high_obs_out, void* stream);
+
+/* hum_hier_reset with resetFromFrame's startFromRef / initVel switches (HUM_RESET_* flags). */
+int hum_hier_reset_ex(hum_env* env, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
+                      uint32_t flags, float* high_obs_out, void* stream);
 
 /* HierarchicalHumanoidEnv.step(action_dict) (hier_env.py:355-366, 538-641) for all lanes: each lane applies the
  * action of the agent it expects (the one that received an observation; `agent` (device u8 [n], 1 = high, 0 = low,

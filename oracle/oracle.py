@@ -201,6 +201,17 @@ class LaneRNG:
         self.counter += 1
         return int(v)
 
+    def joint_noise(self):
+        """flat_env.reset()'s WalkerBase.robot_specific_reset joint positions U(-0.1, 0.1) (XML dof order), from
+        the robot's own np_random: a stream apart from the env draws (key' = splitmix64(key ^ salt), counters
+        (env counter << 5) | dof); the env counter does not advance."""
+        k2 = splitmix64(self.key ^ 0xD1B54A32D192ED03)
+        out = []
+        for d in range(ND):
+            x = splitmix64((k2 + ((self.counter << 5) | d)) & M64)
+            out.append(-0.1 + (0.1 - -0.1) * ((x >> 11) * 2.0 ** -53))
+        return np.array(out)
+
 
 # ----------------------------------------------------------------------------------------- pybullet restatements
 def euler_from_quaternion(q):
@@ -366,6 +377,8 @@ class OracleLowLevelEnv:
         # (all 17 are overwritten below when startFromRef)
         self.state[:] = 0
         self.state[6] = 1.0
+        if not startFromRef:
+            self.state[13:30] = self.rng.joint_noise()
         self.cur_timestep = 0
         if self.usePredefinedTarget:
             self.predefinedTargetIndex = 0

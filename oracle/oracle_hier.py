@@ -118,6 +118,8 @@ class OracleHierEnv:
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :259-319
         self.state[:] = 0
         self.state[6] = 1.0
+        if not startFromRef:
+            self.state[13:30] = self.rng.joint_noise()
         self.cur_timestep = 0
         if self.usePredefinedTarget:
             self.predefinedTargetIndex = 0

@@ -159,6 +159,28 @@ def test_hier_reset_matches_oracle(precision):
     env.close()
 
 
+@pytest.mark.parametrize("start_from_ref,init_vel", [(False, True), (True, False), (False, False)])
+def test_hier_reset_from_frame_switches_match_oracle(start_from_ref, init_vel):
+    """resetFromFrame(startFromRef, initVel) of the two-level env (hier_env.py:259-319)."""
+    clip = load_clip("motion09_03")
+    n = 24
+    env = HierVecEnv(n, seed=78, precision="fp64")
+    env.reset()
+    yaw = np.linspace(-60, 60, n)
+    oh = env.reset(start_frame=torch.full((n,), 9, dtype=torch.int32, device="cuda"),
+                   reset_yaw=torch.as_tensor(yaw, device="cuda"), start_from_ref=start_from_ref,
+                   init_vel=init_vel).cpu().numpy()
+    phys, book = env.get_state()
+    env.close()
+    for i in range(n):
+        o = OH.OracleHierEnv(clip, seed=78, lane=i)
+        o.reset()
+        ref = o.resetFromFrame(9, resetYaw=yaw[i], startFromRef=start_from_ref, initVel=init_vel)
+        assert book[i, N.BK["frame"]] == o.selected_motion_frame
+        np.testing.assert_allclose(phys[i], o.state, atol=1e-12, rtol=0)
+        np.testing.assert_allclose(oh[i], ref[HIGH], atol=1e-6, rtol=1e-6)
+
+
 def test_hier_rollout_at_scale():
     """4096 lanes x 120 auto-reset agent transitions with random high/low actions: protocol invariants."""
     n = 4096

@@ -419,3 +419,31 @@ def test_numpy_semantics_alive_threshold(precision):
                 else -1.0 for x in obs0]
         np.testing.assert_array_equal(alive, want)
         env.close()
+
+
+@pytest.mark.parametrize("kernel", [1, 0])
+@pytest.mark.parametrize("start_from_ref,init_vel", [(False, True), (True, False), (False, False)])
+def test_reset_from_frame_switches_match_oracle(start_from_ref, init_vel, kernel):
+    """resetFromFrame(startFromRef, initVel) (low_level_env.py:247-305): startFromRef=False keeps the frame and
+    leaves the joints at flat_env.reset()'s U(-0.1, 0.1); initVel=False gives no starting base velocity."""
+    clip = load_clip("motion09_03")
+    n = 32
+    env = HumanoidVecEnv(n, clips=(clip,), seed=77, precision="fp64", kernel=kernel)
+    env.reset()
+    yaw = np.linspace(-60, 60, n)
+    obs = env.reset(start_frame=torch.full((n,), 12, dtype=torch.int32, device="cuda"),
+                    reset_yaw=torch.as_tensor(yaw, device="cuda"), start_from_ref=start_from_ref,
+                    init_vel=init_vel).cpu().numpy()
+    phys, book = env.get_state()
+    env.close()
+    for i in range(n):
+        o = O.OracleLowLevelEnv(clip, seed=77, lane=i)
+        o.reset()
+        ref = o.resetFromFrame(12, resetYaw=yaw[i], startFromRef=start_from_ref, initVel=init_vel)
+        assert book[i, N.BK["frame"]] == o.frame
+        np.testing.assert_allclose(phys[i], o.state, atol=1e-12, rtol=0)
+        np.testing.assert_allclose(obs[i], ref, atol=1e-6, rtol=1e-6)
+        if not init_vel or not start_from_ref:
+            assert (phys[i, 7:10] == 0).all()
+        if not start_from_ref:
+            assert (np.abs(phys[i, 13:30]) <= 0.1).all() and (phys[i, 30:47] == 0).all()
