@@ -31,6 +31,9 @@ int fail(int code, const std::string& msg) {
 
 }  // namespace
 
+// messages of host-side pieces in other translation units (clip_csv.cpp) go to hum_last_error() too
+__attribute__((visibility("hidden"))) void hum_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
 
 // ======================================================================================= C-ABI
 struct hum_env {
@@ -615,17 +618,6 @@ int hum_sync(hum_env* e) {
 
 int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
 
-#ifdef HUM_CHECK_LINKS
-int hum_debug_check(unsigned* out8, int reset) {
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_check), 8 * sizeof(unsigned)));
-    if (reset) {
-        unsigned z[8] = {0};
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_check), z, sizeof z));
-    }
-    return HUM_OK;
-}
-#endif
 
 #ifdef HUM_WLOG_ON
 int hum_debug_wave_log(unsigned* out, int nblocks, int reset) {   // diag: per-block work log (WLOG_W u32 each)

@@ -147,7 +147,7 @@ __device__ inline void joint_noise(const Book& b, T* st) {
 // ----------------------------------------------------------------------------------- reset
 // LowLevelHumanoidEnv.reset() / resetFromFrame() (low_level_env.py:224-305)
 template <typename T>
-__device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* obs,
+__device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* obs,
                            unsigned& ef, const T* scs = nullptr) {   // scs: the reset pose's hinge sin / cos
     const ClipDev& c = a.clips[b.clip];
     const bool ref = !(a.reset_flags & HUM_RESET_NO_REF_POSE);                // startFromRef
@@ -224,7 +224,7 @@ __device__ void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_fram
 
 // Post-physics part of step (low_level_env.py:481-526) + optional auto-reset; stores state, book, outputs.
 template <typename T>
-__device__ void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef, const T* scs = nullptr,
+__device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef, const T* scs = nullptr,
                           bool* defer_reset = nullptr) {   // defer_reset: the caller runs the auto-reset and the store
     const ClipDev& c = a.clips[b.clip];
     float obs[HUM_NOBS];
@@ -340,7 +340,7 @@ __device__ inline void hier_high_obs(const float* obs42, const Book& b, double y
 
 // reset() / resetFromFrame() (hier_env.py:235-319)
 template <typename T>
-__device__ void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* o44,
+__device__ __attribute__((always_inline)) void hier_reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* o44,
                                 unsigned& ef) {
     const ClipDev& c = a.clips[b.clip];
     const bool ref = !(a.reset_flags & HUM_RESET_NO_REF_POSE);
@@ -423,7 +423,7 @@ __device__ inline float hier_update_reward_high(Book& b) {
 // step(action_dict) (hier_env.py:355-366) -> high_level_step (:538-571) or low_level_step (:583-641), after the
 // physics of a low step; stores state/book and writes the dict-shaped outputs.
 template <typename T>
-__device__ void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsigned& ef, const T* scs = nullptr) {
+__device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsigned& ef, const T* scs = nullptr) {
     const ClipDev& c = a.clips[b.clip];
     b.robot_pos[0] = b.bxy[0]; b.robot_pos[1] = b.bxy[1]; b.robot_pos[2] = 0;   // step(): :358-361
     float obs[HUM_NOBS], js[NDOF], o44[HUM_NOBS_HIGH];

@@ -11,6 +11,8 @@ from dataclasses import dataclass
 import numpy as np
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "clips")
+# the reference's CSV quadruples ("Joints CSV With Hand/", read by low_level_env.py:58-70), shipped as data
+CSV_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "csv")
 CLIP_NAMES = ["motion02_04", "motion08_03", "motion09_03", "motion13_13"]
 
 # joint_map of LowLevelHumanoidEnv (low_level_env.py:86-101): env joint -> CSV column, dict order.
@@ -63,3 +65,24 @@ def load_clip(name_or_path):
         off += rows * cols * 8
         arrs.append(a)
     return Clip(meta["clip"], *arrs, meta["joint_cols"], meta["ep_cols"])
+
+
+JOINT_COLS = ["rightHipX", "rightHipY", "rightHipZ", "rightKnee", "leftHipX", "leftHipY", "leftHipZ", "leftKnee",
+              "rightShoulderX", "rightShoulderY", "rightElbow", "leftShoulderX", "leftShoulderY", "leftElbow"]
+EP_COLS = ["%s_%sposition" % (p, a) for p in ("LeftLeg", "LeftFoot", "RightLeg", "RightFoot", "Head", "LeftForeArm",
+                                              "LeftHand", "RightForeArm", "RightHand") for a in "XYZ"]
+
+
+def load_clip_csv(name, csv_dir=CSV_DIR):
+    """Runtime ingestion of the reference's 4-CSV clip format through the native loader (libhumenv.so,
+    hum_clip_csv_parse: pandas' float converter, bit-identical tables; no pandas needed)."""
+    import ctypes
+    from . import _native as N
+    L = N.lib()
+    d, n = csv_dir.encode(), name.encode()
+    sz = (ctypes.c_int32 * 4)()
+    N.check(L.hum_clip_csv_sizes(d, n, sz), "hum_clip_csv_sizes")
+    arrs = [np.zeros((sz[k], 27 if k == 3 else 14)) for k in range(4)]
+    dp = ctypes.POINTER(ctypes.c_double)
+    N.check(L.hum_clip_csv_parse(d, n, *[a.ctypes.data_as(dp) for a in arrs]), "hum_clip_csv_parse")
+    return Clip(name, *arrs, list(JOINT_COLS), list(EP_COLS))

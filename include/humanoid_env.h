@@ -168,6 +168,17 @@ int hum_destroy(hum_env* env);
  * RightHand} x {X,Y,Z} (27).  max_frame = n_pos - 1 (:80-82). */
 int hum_set_clip(hum_env* env, int32_t clip_id, const double* pos, int32_t n_pos, const double* vel, int32_t n_vel,
                  const double* rel, int32_t n_rel, const double* ep, int32_t n_ep);
+/* Runtime clip ingestion (host code): parse the reference's CSV quadruple <dir>/<name>{JointPosRad,
+ * JointSpeedRadSec,JointPosRadRelative,JointVecFromHip}.csv (low_level_env.py:58-70) with pandas' default float
+ * converter (bit-identical tables), columns by header name in hum_set_clip's order.
+ *   hum_clip_csv_sizes: rows of the four tables -> sizes4[4] (no GPU needed)
+ *   hum_clip_csv_parse: the tables into caller buffers sized from hum_clip_csv_sizes (no GPU needed)
+ *   hum_load_clip_csv: parse + hum_set_clip(env, clip_id, ...)
+ * Errors: HUM_ERR_ARG with the reason in hum_last_error(). */
+int hum_clip_csv_sizes(const char* dir, const char* name, int32_t* sizes4);
+int hum_clip_csv_parse(const char* dir, const char* name, double* pos, double* vel, double* rel, double* ep);
+int hum_load_clip_csv(hum_env* env, int32_t clip_id, const char* dir, const char* name);
+
 /* clip id per lane (host array of n_lanes); default all 0 */
 int hum_set_lane_clips(hum_env* env, const int32_t* clip_of_lane);
 /* per-lane HUM_MODE_* bits (host array of n_lanes) */

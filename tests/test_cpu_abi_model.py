@@ -195,3 +195,35 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     finally:
         monkeypatch.delenv("ILRL_AMD_LIB")
         importlib.reload(nat)
+
+
+def test_runtime_csv_clip_loader_is_bit_identical_to_pandas():
+    """hum_clip_csv_parse (csrc/clip_csv.cpp, pandas' default float converter restated) reproduces the tables
+    the reference env reads with pandas (the packed .clip files were made by pandas.read_csv,
+    tools/pack_clips.py) bit for bit on all four clips; a correctly rounded parser would not."""
+    from ilrl_amd.clips import CLIP_NAMES, CSV_DIR, load_clip, load_clip_csv
+    for name in CLIP_NAMES:
+        a, b = load_clip_csv(name), load_clip(name)
+        for t in ("pos", "vel", "rel", "ep"):
+            x, y = getattr(a, t), getattr(b, t)
+            assert x.shape == y.shape, (name, t)
+            assert (x.view(np.int64) == y.view(np.int64)).all(), (name, t)
+        assert a.joint_cols == b.joint_cols and a.ep_cols == b.ep_cols
+    # the shipped CSVs are the reference's: first value of motion09_03 JointPosRad, which pandas' converter reads
+    # one ulp away from the correctly rounded -0.07757971159472256
+    v = load_clip_csv("motion09_03").pos[0, 0]
+    assert v != -0.07757971159472256 and abs(v - (-0.07757971159472256)) < 1e-16
+
+
+def test_runtime_csv_clip_loader_errors(tmp_path):
+    from ilrl_amd.clips import load_clip_csv
+    with pytest.raises(N.NativeError, match="cannot open"):
+        load_clip_csv("motion99_99")
+    import shutil
+    from ilrl_amd.clips import CSV_DIR
+    for suf in ("JointPosRad", "JointSpeedRadSec", "JointPosRadRelative", "JointVecFromHip"):
+        shutil.copy(os.path.join(CSV_DIR, "motion09_03%s.csv" % suf), tmp_path / ("bad%s.csv" % suf))
+    p = tmp_path / "badJointSpeedRadSec.csv"
+    p.write_text(p.read_text() + "1.0,2.0\n")   # ragged row
+    with pytest.raises(N.NativeError, match="ragged"):
+        load_clip_csv("bad", str(tmp_path))

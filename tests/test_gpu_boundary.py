@@ -87,3 +87,27 @@ def test_graph_recaptured_after_predefined_targets_change():
         np.testing.assert_array_equal(b0, b1)
     for e in envs:
         e.close()
+
+
+def test_load_clip_csv_on_device_equals_packed_clip():
+    """hum_load_clip_csv (runtime 4-CSV ingestion, pandas-identical parse) uploads the same tables as the
+    packed .clip path: identical rollouts."""
+    from ilrl_amd.clips import CSV_DIR
+    n = 64
+    envs = [HumanoidVecEnv(n, clips=("motion08_03", "motion13_13"), seed=4) for _ in range(2)]
+    for cid, name in enumerate(("motion08_03", "motion13_13")):
+        assert N.lib().hum_load_clip_csv(envs[1].h, cid, CSV_DIR.encode(), name.encode()) == 0
+    g = torch.Generator(device="cuda").manual_seed(6)
+    acts = [(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1).contiguous() for _ in range(20)]
+    for e in envs:
+        e.reset()
+        for a in acts:
+            e.step(a, autoreset=True)
+    p0, b0 = envs[0].get_state()
+    p1, b1 = envs[1].get_state()
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(b0, b1)
+    assert N.lib().hum_load_clip_csv(envs[1].h, 0, CSV_DIR.encode(), b"nope") != 0
+    assert b"cannot open" in N.lib().hum_last_error()
+    for e in envs:
+        e.close()
