@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--hier", action="store_true",
                     help="config 5: HierarchicalHumanoidEnv two-level rollout (hum_hier_step), clip motion09_03")
     ap.add_argument("--gather-every", type=int, default=0, help="multi-GPU: trajectory all-gather every K steps")
+    ap.add_argument("--policy", action="store_true",
+                    help="closed loop: actions from the on-GPU policy network (random-init weights, exploration "
+                         "noise) inside the timed loop, SURVEY 8(f) rank 2")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / parity side measurements")
     return ap.parse_args()
 
@@ -159,7 +162,16 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys):
         env = HumanoidVecEnv(n, clips=clips, seed=0, device=dev.index, lane_offset=rank * n, precision=precision,
                              block_size=a.block, **phys)
         step = lambda s: env.step(pool[s % 16], autoreset=True)
+        if a.policy:
+            from ilrl_amd.policy import DevicePolicy
+            pol = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
+            actbuf = torch.zeros(n, 17, device=dev)
+
+            def step(s):
+                pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s, out=actbuf)
+                return env.step(actbuf, autoreset=True)
     env.reset()
+    env.done.zero_()
     for w in range(warmup):
         step(w)
     gather_s = 0.0
@@ -259,7 +271,9 @@ def main():
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
             "config": {"workload": ("HumanoidBulletEnv-v0-Hier two-level rollout (high heading every 5 low steps), "
                                     if a.hier else "HumanoidBulletEnv-v0-Low step+reward, ") +
-                                   "%s, %d envs/GPU, uniform random actions, auto-reset" % (a.clip, n),
+                                   "%s, %d envs/GPU, %s, auto-reset" % (
+                                       a.clip, n, "on-GPU policy actions (random-init 70-256-256-17 tanh MLP + "
+                                       "Gaussian exploration) in the loop" if a.policy else "uniform random actions"),
                        "envs_per_gpu": n, "clip": a.clip,
                        "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -281,7 +295,7 @@ def main():
         if world > 1 and a.gather_every:
             out["gather"] = {"every": a.gather_every, "seconds": gather_s,
                              "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1)}
-        if world == 1 and not a.no_secondary and not a.hier:
+        if world == 1 and not a.no_secondary and not a.hier and not a.policy:
             from ilrl_amd.clips import CLIP_NAMES
             clips = tuple(CLIP_NAMES) if a.clip == "all" else (a.clip,)
             out["parity"] = parity_sample(env, clips)

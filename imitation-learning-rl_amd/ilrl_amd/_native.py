@@ -36,7 +36,8 @@ EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_creat
            "hum_set_lane_clips", "hum_set_lane_modes", "hum_set_predefined_targets", "hum_reset", "hum_step",
            "hum_step_graph", "hum_get_aux", "hum_get_state", "hum_set_state", "hum_get_parts",
            "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step",
-           "hum_reset_ex", "hum_hier_reset_ex", "hum_clip_csv_sizes", "hum_clip_csv_parse", "hum_load_clip_csv"]
+           "hum_reset_ex", "hum_hier_reset_ex", "hum_clip_csv_sizes", "hum_clip_csv_parse", "hum_load_clip_csv",
+           "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout"]
 
 
 class HumConfig(ctypes.Structure):
@@ -86,6 +87,10 @@ def lib():
     L.hum_clip_csv_sizes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]
     L.hum_clip_csv_parse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, dp, dp, dp, dp]
     L.hum_load_clip_csv.argtypes = [vp, i32, ctypes.c_char_p, ctypes.c_char_p]
+    L.hum_policy_create.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(vp)]
+    L.hum_policy_destroy.argtypes = [vp]
+    L.hum_policy_act.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, u64, vp]
+    L.hum_rollout.argtypes = [vp, vp, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.hum_hier_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.hum_step.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, vp]
     L.hum_hier_reset.argtypes = [vp, vp, vp, vp, vp, vp]

@@ -1,0 +1,128 @@
+"""On-GPU policy inference and a device-resident sampler loop over the C-ABI
+(include/humanoid_env.h: hum_policy_create / hum_policy_act / hum_rollout).
+
+The network is the reference's PPO policy (train_config.py:107-111: RLlib 1.2 FullyConnectedNetwork,
+fcnet_hiddens [256, 256], fcnet_activation tanh, free_log_std True): action mean =
+W3 tanh(W2 tanh(W1 obs + b1) + b2) + b3, sampled as DiagGaussian(mean, exp(log_std)) and clipped to the
+action Box (RLlib clip_actions).  Weights come from `from_rllib_weights` (the dict a TF policy's
+get_weights() returns, exported where Ray runs) or `random_init` (RLlib's normc initialisers; benchmarks).
+The reference's trained checkpoints are pickles that the safe loaders refuse, so no
+trained weights ship here.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+H = 256
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _normc(rng, shape, std):
+    """RLlib's normc_initializer: normal columns scaled to norm `std`."""
+    w = rng.standard_normal(shape).astype(np.float32)
+    return (w * std / np.sqrt(np.square(w).sum(axis=0, keepdims=True))).astype(np.float32)
+
+
+class DevicePolicy:
+    """The policy network on one GPU (weights fp32, TF kernel layout [in][out])."""
+
+    KEYS = ("w1", "b1", "w2", "b2", "w3", "b3", "log_std")
+
+    def __init__(self, weights, device=0, seed=0):
+        import torch
+        self.torch = torch
+        self.device = torch.device("cuda", device)
+        shapes = {"w1": (N.HUM_NOBS, H), "b1": (H,), "w2": (H, H), "b2": (H,), "w3": (H, N.HUM_NACT),
+                  "b3": (N.HUM_NACT,), "log_std": (N.HUM_NACT,)}
+        self.w = {}
+        for k in self.KEYS:
+            a = np.ascontiguousarray(weights.get(k, np.zeros(shapes[k])), dtype=np.float32)
+            if a.shape != shapes[k]:
+                raise ValueError("%s: shape %s, expected %s" % (k, a.shape, shapes[k]))
+            self.w[k] = a
+        h = ctypes.c_void_p()
+        N.check(N.lib().hum_policy_create(device, *[_fp(self.w[k]) for k in self.KEYS], ctypes.c_uint64(seed),
+                                          ctypes.byref(h)), "hum_policy_create")
+        self.h = h
+
+    @classmethod
+    def random_init(cls, seed=0, device=0, log_std=-0.5):
+        rng = np.random.default_rng(seed)
+        w = {"w1": _normc(rng, (N.HUM_NOBS, H), 1.0), "b1": np.zeros(H), "w2": _normc(rng, (H, H), 1.0),
+             "b2": np.zeros(H), "w3": _normc(rng, (H, N.HUM_NACT), 0.01), "b3": np.zeros(N.HUM_NACT),
+             "log_std": np.full(N.HUM_NACT, log_std)}
+        return cls(w, device=device, seed=seed)
+
+    @classmethod
+    def from_rllib_weights(cls, weights, device=0, seed=0):
+        """From a TF FullyConnectedNetwork's get_weights() dict (variable name -> array): the policy branch
+        fc_1, fc_2, fc_out and the free log_std variable (value-branch variables are ignored).  The name mapping
+        follows RLlib 1.2's naming; it is not exercised against a real checkpoint here (no Ray in this image)."""
+        def pick(sub):
+            hits = [k for k in weights if sub in k and "value" not in k]
+            if len(hits) != 1:
+                raise KeyError("expected exactly one variable matching %r, got %s" % (sub, hits))
+            return np.asarray(weights[hits[0]])
+        w = {"w1": pick("fc_1/kernel"), "b1": pick("fc_1/bias"), "w2": pick("fc_2/kernel"), "b2": pick("fc_2/bias"),
+             "w3": pick("fc_out/kernel"), "b3": pick("fc_out/bias"), "log_std": pick("log_std")}
+        w["log_std"] = w["log_std"].reshape(-1)
+        return cls(w, device=device, seed=seed)
+
+    def close(self):
+        if getattr(self, "h", None):
+            N.lib().hum_policy_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def act(self, obs, obs_reset=None, done=None, explore=False, step=0, out=None, mean_out=None):
+        """actions [n,17] (device) for device observations obs [n,70] (done lanes read obs_reset)."""
+        t = self.torch
+        n = obs.shape[0]
+        act = out if out is not None else t.empty(n, N.HUM_NACT, dtype=t.float32, device=self.device)
+        p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
+        N.check(N.lib().hum_policy_act(self.h, p(obs), p(obs_reset), p(done), n, p(act), p(mean_out), None,
+                                       int(bool(explore)), ctypes.c_uint64(step), self._stream()), "hum_policy_act")
+        return act
+
+    def rollout(self, venv, k, explore=True, step0=0, trajectories=True):
+        """k sampler steps (policy -> env step with auto-reset) on venv's lanes, all on the device with no host
+        round trip.  venv.obs must hold the current observation (after venv.reset()).  Returns the trajectory
+        tensors {obs [k,n,70] (policy inputs), actions [k,n,17], rewards [k,n], dones [k,n]} (or {})."""
+        t = self.torch
+        n = venv.n
+        if not hasattr(venv, "_act_buf"):
+            venv._act_buf = t.zeros(n, N.HUM_NACT, dtype=t.float32, device=venv.device)
+        tr = {}
+        if trajectories:
+            tr = {"obs": t.empty(k, n, N.HUM_NOBS, dtype=t.float32, device=venv.device),
+                  "actions": t.empty(k, n, N.HUM_NACT, dtype=t.float32, device=venv.device),
+                  "rewards": t.empty(k, n, dtype=t.float32, device=venv.device),
+                  "dones": t.empty(k, n, dtype=t.uint8, device=venv.device)}
+        p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
+        N.check(N.lib().hum_rollout(venv.h, self.h, k, int(bool(explore)), ctypes.c_uint64(step0), p(venv.obs),
+                                    p(venv.obs_reset), p(venv.done), p(venv.reward), p(venv._act_buf),
+                                    p(tr.get("obs")), p(tr.get("actions")), p(tr.get("rewards")), p(tr.get("dones")),
+                                    venv._stream()), "hum_rollout")
+        return tr
+
+
+def reference_mean(w, obs):
+    """The same network in plain PyTorch fp32 (tests' reference): the action mean."""
+    import torch
+    T = lambda k: torch.as_tensor(w[k], dtype=torch.float32, device=obs.device)
+    h1 = torch.tanh(obs @ T("w1") + T("b1"))
+    h2 = torch.tanh(h1 @ T("w2") + T("b2"))
+    return h2 @ T("w3") + T("b3")

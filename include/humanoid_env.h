@@ -230,6 +230,28 @@ int hum_hier_step(hum_env* env, const float* high_act, const float* low_act, con
                   float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
                   uint32_t flags, float* high_obs_reset, void* stream);
 
+/* ---- On-GPU policy inference: the reference's PPO policy network (train_config.py:107-111,
+ * RLlib FullyConnectedNetwork, fcnet_hiddens [256, 256], tanh, free_log_std) evaluated on the env's device
+ * buffers, so a sampler loop needs no host round trip.  Weights: host float32, TF kernel layout [in][out]:
+ * w1 [70,256], b1 [256], w2 [256,256], b2 [256], w3 [256,17], b3 [17], log_std [17] (NULL = zeros). */
+typedef struct hum_policy hum_policy;
+int hum_policy_create(int32_t device, const float* w1, const float* b1, const float* w2, const float* b2,
+                      const float* w3, const float* b3, const float* log_std, uint64_t seed, hum_policy** out);
+int hum_policy_destroy(hum_policy* policy);
+/* actions [n,17] (device) = clip(mean + explore * exp(log_std) * N(0,1), -1, 1) (RLlib clip_actions) for the
+ * observations obs [n,70]; lanes with done[i] != 0 read obs_reset[i] instead (the auto-reset observation; both
+ * NULL = obs only).  mean_out [n,17] and obs_in_out [n,70] (the observation rows used) are optional.  Noise is
+ * counter-based: (seed, lane, step, action index). */
+int hum_policy_act(hum_policy* policy, const float* obs, const float* obs_reset, const uint8_t* done, int32_t n,
+                   float* actions, float* mean_out, float* obs_in_out, int32_t explore, uint64_t step, void* stream);
+/* k sampler steps (policy -> hum_step with HUM_STEP_AUTORESET) on `stream` with no host round trip.  obs,
+ * obs_reset, done, reward: the env-step buffers (device [n,70], [n,70], [n], [n]); on entry obs holds the current
+ * observation and done the previous step's flags (zeros after a reset); act_buf [n,17] scratch.  Optional device
+ * trajectory outputs: obs_traj [k,n,70] (the policy inputs), act_traj [k,n,17], rew_traj [k,n], done_traj [k,n]. */
+int hum_rollout(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
+                float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
+                float* rew_traj, uint8_t* done_traj, void* stream);
+
 /* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
 int hum_get_aux(hum_env* env, float* aux_out, void* stream);
 

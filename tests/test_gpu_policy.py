@@ -1,0 +1,95 @@
+"""On-GPU policy inference (csrc/policy.hip, v_mfma_f32_16x16x4_f32) vs a plain PyTorch fp32 reference of the
+same network, and the device-resident rollout loop vs the same loop driven step by step from Python.
+
+Tolerance: the MFMA computes each output as a k-ordered fp32 fma chain, torch's matmul in another order; after
+two tanh layers the action means agree to 2e-5 absolute (fp32 rounding of K = 256 dot products)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from ilrl_amd import _native as N  # noqa: E402
+from ilrl_amd.policy import DevicePolicy, reference_mean  # noqa: E402
+from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+
+@pytest.mark.parametrize("n", [1, 17, 4096])
+def test_policy_mean_matches_torch_fp32(n):
+    pol = DevicePolicy.random_init(seed=3)
+    pol.w["b1"][:] = np.linspace(-0.3, 0.3, 256)   # non-zero biases exercise every term
+    pol.close()
+    pol = DevicePolicy(pol.w, seed=3)
+    g = torch.Generator(device="cuda").manual_seed(n)
+    obs = (torch.randn(n, 70, device="cuda", generator=g) * 2).contiguous()
+    mean = torch.empty(n, 17, device="cuda")
+    act = pol.act(obs, mean_out=mean)
+    ref = reference_mean(pol.w, obs)
+    assert (mean - ref).abs().max().item() < 2e-5
+    torch.testing.assert_close(act, ref.clamp(-1, 1), atol=2e-5, rtol=0)
+    pol.close()
+
+
+def test_policy_done_lanes_read_reset_obs_and_exploration_noise():
+    n = 2048
+    pol = DevicePolicy.random_init(seed=5, log_std=-2.0)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    obs = torch.randn(n, 70, device="cuda", generator=g)
+    obs_r = torch.randn(n, 70, device="cuda", generator=g)
+    done = (torch.rand(n, device="cuda", generator=g) < 0.3).to(torch.uint8)
+    mean = torch.empty(n, 17, device="cuda")
+    pol.act(obs, obs_r, done, mean_out=mean)
+    want = torch.where(done.bool()[:, None], obs_r, obs)
+    assert (mean - reference_mean(pol.w, want)).abs().max().item() < 2e-5
+    a1 = pol.act(want, explore=True, step=7, mean_out=mean)
+    a2 = pol.act(want, explore=True, step=7)
+    a3 = pol.act(want, explore=True, step=8)
+    assert torch.equal(a1, a2) and not torch.equal(a1, a3)   # counter-based: (seed, lane, step, index)
+    z = ((a1 - mean) / np.exp(-2.0))[(a1.abs() < 1)]        # unclipped samples: standard normal noise
+    assert abs(z.mean().item()) < 0.02 and abs(z.std().item() - 1) < 0.02
+    pol.close()
+
+
+def test_rollout_equals_python_loop():
+    """hum_rollout (policy -> step with auto-reset, k launches pairs on one stream) == the same loop from Python."""
+    n, k = 512, 24
+    pol = DevicePolicy.random_init(seed=9)
+    envs = [HumanoidVecEnv(n, clips=("motion02_04",), seed=2) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        e.done.zero_()
+    tr = pol.rollout(envs[0], k, explore=True, step0=100)
+    e = envs[1]
+    act = torch.empty(n, 17, device="cuda")
+    for t in range(k):
+        inp = torch.where(e.done.bool()[:, None], e.obs_reset, e.obs).clone()
+        torch.testing.assert_close(tr["obs"][t], inp, atol=0, rtol=0)
+        pol.act(e.obs, e.obs_reset, e.done, explore=True, step=100 + t, out=act)
+        torch.testing.assert_close(tr["actions"][t], act, atol=0, rtol=0)
+        e.step(act, autoreset=True)
+        torch.testing.assert_close(tr["rewards"][t], e.reward, atol=0, rtol=0)
+        assert torch.equal(tr["dones"][t], e.done)
+    p0, b0 = envs[0].get_state()
+    p1, b1 = envs[1].get_state()
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(b0, b1)
+    assert tr["dones"].sum().item() > 0
+    for x in envs:
+        x.close()
+    pol.close()
+
+
+def test_rllib_weight_names():
+    """from_rllib_weights picks the policy branch of an RLlib 1.2 TF FullyConnectedNetwork weight dict."""
+    rng = np.random.default_rng(0)
+    d = {"default_policy/fc_1/kernel": rng.standard_normal((70, 256)), "default_policy/fc_1/bias": np.zeros(256),
+         "default_policy/fc_2/kernel": rng.standard_normal((256, 256)), "default_policy/fc_2/bias": np.zeros(256),
+         "default_policy/fc_out/kernel": rng.standard_normal((256, 17)), "default_policy/fc_out/bias": np.zeros(17),
+         "default_policy/log_std": np.zeros(17), "default_policy/fc_value_1/kernel": np.zeros((70, 256)),
+         "default_policy/value_out/kernel": np.zeros((256, 1))}
+    pol = DevicePolicy.from_rllib_weights(d)
+    np.testing.assert_array_equal(pol.w["w2"], d["default_policy/fc_2/kernel"].astype(np.float32))
+    pol.close()
