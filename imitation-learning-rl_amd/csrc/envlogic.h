@@ -41,6 +41,7 @@ struct Book {   // per-lane bookkeeping (mirrors HUM_BK_* in include/humanoid_en
     int frame, timestep, pred_idx, clip;
     unsigned rng_ctr, mode;
     unsigned long long rng_key;
+    unsigned long long terrain_key;   // HUM_TERRAIN_RANDOM_BLOCKS: the lane's current terrain
     double target[3], srp[3], robot_pos[3], sep[3];
     double hldt, wt[2], lts;
     double dj, dvj, bps, es, jls, alive, dlts;

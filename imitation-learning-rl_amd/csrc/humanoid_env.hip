@@ -49,6 +49,11 @@ struct hum_env {
     double* pred;
     int npred;
     unsigned* eflags;
+    // ground (hum_set_terrain)
+    int terrain;
+    float* hf;
+    int hf_w, hf_l;
+    double hf_s[3], hf_o[3], hf_mid;
     hipGraphExec_t graph;
     int graph_k;
     const void* graph_key[6];
@@ -87,6 +92,12 @@ KArgs make_args(hum_env* e) {
     a.P.self_collision = c.self_collision;
     a.P.joint_damping = c.joint_damping;
     a.P.lds_rows = lds_rows_of(c);
+    a.P.terrain = e->terrain;
+    a.P.hf = e->hf;
+    a.P.hf_w = e->hf_w;
+    a.P.hf_l = e->hf_l;
+    for (int k = 0; k < 3; k++) { a.P.hf_s[k] = e->hf_s[k]; a.P.hf_o[k] = e->hf_o[k]; }
+    a.P.hf_mid = e->hf_mid;
     a.hier = c.hier;
     a.np1 = c.numpy_semantics == HUM_NUMPY_1;
     a.clips = e->clips_dev;
@@ -226,6 +237,7 @@ int hum_destroy(hum_env* e) {
     (void)hipFree(e->eflags);
     (void)hipFree(e->clips_dev);
     (void)hipFree(e->pred);
+    (void)hipFree(e->hf);
     for (int k = 0; k < HUM_MAX_CLIPS; k++) (void)hipFree(e->clip_dev[k]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -283,6 +295,49 @@ int hum_set_predefined_targets(hum_env* e, const double* xyz, int32_t n) {
         HIPCHK(hipMalloc((void**)&e->pred, n * 3 * sizeof(double)));
         HIPCHK(hipMemcpy(e->pred, xyz, n * 3 * sizeof(double), hipMemcpyHostToDevice));
     }
+    return HUM_OK;
+}
+
+int hum_set_terrain(hum_env* e, int32_t mode, const float* heights, int32_t w, int32_t l, const double* scale3,
+                    const double* origin3) {
+    if (!e) return fail(HUM_ERR_ARG, "hum_set_terrain: null env");
+    if (mode != HUM_TERRAIN_PLANE && mode != HUM_TERRAIN_HEIGHTFIELD && mode != HUM_TERRAIN_RANDOM_BLOCKS)
+        return fail(HUM_ERR_ARG, "hum_set_terrain: unknown mode");
+    if (mode != HUM_TERRAIN_PLANE && (e->cfg.kernel != 1 || e->cfg.hier || e->cfg.envs_per_block != 4))
+        return fail(HUM_ERR_STATE, "hum_set_terrain: terrain needs a low-level handle on the cooperative kernel "
+                                   "(kernel 1, envs_per_block 4)");
+    std::vector<float> h;
+    double s[3] = {1, 1, 1}, o[3] = {0, 0, 0.25}, mid = 0.25;   // CustomScene: scale 1, body at z 0.25
+    int W = 256, L = 256;
+    if (mode == HUM_TERRAIN_HEIGHTFIELD) {
+        if (!heights || !scale3 || !origin3 || w < 2 || l < 2) return fail(HUM_ERR_ARG, "hum_set_terrain: bad heightfield");
+        if (!(scale3[0] >= 0.5 && scale3[1] >= 0.5 && scale3[2] > 0))
+            return fail(HUM_ERR_ARG, "hum_set_terrain: scale x, y must be >= 0.5 and z > 0");
+        W = w;
+        L = l;
+        h.assign(heights, heights + (size_t)w * l);
+        float lo = h[0], hi = h[0];
+        for (float v : h) {
+            if (!std::isfinite(v)) return fail(HUM_ERR_ARG, "hum_set_terrain: non-finite height");
+            lo = v < lo ? v : lo;
+            hi = v > hi ? v : hi;
+        }
+        mid = 0.5 * ((double)lo + (double)hi);   // btHeightfieldTerrainShape m_localOrigin
+        for (int k = 0; k < 3; k++) { s[k] = scale3[k]; o[k] = origin3[k]; }
+    }
+    HIPCHK(hipSetDevice(e->cfg.device));
+    HIPCHK(quiesce(e));   // launches in flight (and a captured graph) hold the old terrain by value
+    if (e->hf) HIPCHK(hipFree(e->hf));
+    e->hf = nullptr;
+    if (mode == HUM_TERRAIN_HEIGHTFIELD) {
+        HIPCHK(hipMalloc((void**)&e->hf, h.size() * sizeof(float)));
+        HIPCHK(hipMemcpy(e->hf, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    e->terrain = mode;
+    e->hf_w = W;
+    e->hf_l = L;
+    for (int k = 0; k < 3; k++) { e->hf_s[k] = s[k]; e->hf_o[k] = o[k]; }
+    e->hf_mid = mid;
     return HUM_OK;
 }
 
@@ -382,14 +437,21 @@ int hum_hier_step(hum_env* e, const float* high_act, const float* low_act, const
 namespace {
 int launch_step(hum_env* e, const KArgs& a, hipStream_t s) {
 #ifdef HUM_DIAG_F32_ONLY   // diagnostic builds (phase timing): only the benchmarked kernel is instantiated
-    if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != 4)
-        return fail(HUM_ERR_ARG, "diagnostic build: only kernel 1, fp32, envs_per_block 4");
-    hipLaunchKernelGGL((step_group_kernel<float, 4>), dim3((e->n + 3) / 4), dim3(4 * GL), 0, s, a);
+#ifndef HUM_DIAG_EPB
+#define HUM_DIAG_EPB 4
+#endif
+    if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != HUM_DIAG_EPB || e->terrain)
+        return fail(HUM_ERR_ARG, "diagnostic build: only kernel 1, fp32, envs_per_block HUM_DIAG_EPB, plane");
+    hipLaunchKernelGGL((step_group_kernel<float, HUM_DIAG_EPB>), dim3((e->n + HUM_DIAG_EPB - 1) / HUM_DIAG_EPB),
+                       dim3(HUM_DIAG_EPB * GL), 0, s, a);
 #else
     if (e->cfg.kernel == 1) {
         const int epb = e->cfg.envs_per_block;
         const dim3 g((e->n + epb - 1) / epb), blk(epb * GL);
-        if (e->cfg.precision) {
+        if (e->terrain != HUM_TERRAIN_PLANE) {   // heightfield ground: its own instantiation (envs_per_block 4)
+            if (e->cfg.precision) hipLaunchKernelGGL((step_group_kernel<double, 4, true>), g, blk, 0, s, a);
+            else hipLaunchKernelGGL((step_group_kernel<float, 4, true>), g, blk, 0, s, a);
+        } else if (e->cfg.precision) {
             if (epb == 4) hipLaunchKernelGGL((step_group_kernel<double, 4>), g, blk, 0, s, a);
             else if (epb == 2) hipLaunchKernelGGL((step_group_kernel<double, 2>), g, blk, 0, s, a);
             else hipLaunchKernelGGL((step_group_kernel<double, 1>), g, blk, 0, s, a);
@@ -511,6 +573,8 @@ int hum_get_state(hum_env* e, double* phys, double* book) {
             o[HUM_BK_CUM_ALIVE] = bd[27 * n + i];
             o[HUM_BK_BODY_XY] = bd[28 * n + i];
             o[HUM_BK_BODY_XY + 1] = bd[29 * n + i];
+            o[HUM_BK_TERRAIN_KEY_LO] = (double)(unsigned)bi[11 * n + i];
+            o[HUM_BK_TERRAIN_KEY_HI] = (double)(unsigned)bi[12 * n + i];
         }
     }
     return HUM_OK;
@@ -573,6 +637,8 @@ int hum_set_state(hum_env* e, const double* phys, const double* book) {
             bd[27 * n + i] = o[HUM_BK_CUM_ALIVE];
             bd[28 * n + i] = o[HUM_BK_BODY_XY];
             bd[29 * n + i] = o[HUM_BK_BODY_XY + 1];
+            bi[11 * n + i] = (int)(unsigned)o[HUM_BK_TERRAIN_KEY_LO];
+            bi[12 * n + i] = (int)(unsigned)o[HUM_BK_TERRAIN_KEY_HI];
         }
         HIPCHK(hipMemcpy(e->d.bi, bi.data(), bi.size() * sizeof(int), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->d.bd, bd.data(), bd.size() * sizeof(double), hipMemcpyHostToDevice));

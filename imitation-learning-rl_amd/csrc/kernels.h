@@ -16,8 +16,8 @@
 namespace hkk {
 using namespace hk;
 
-constexpr int NBOOK_I = 11;   // frame, timestep, pred_idx, clip, rng_ctr, mode, rng key lo, rng key hi
-                              // | hier: level_rem, n_high, expect_high
+constexpr int NBOOK_I = 13;   // frame, timestep, pred_idx, clip, rng_ctr, mode, rng key lo, rng key hi
+                              // | hier: level_rem, n_high, expect_high | terrain key lo, hi (terrain 2)
 constexpr int NBOOK_D = 30;   // target3 srp3 robot_pos3 sep3 hldt wt2 lts dj dvj bps es jls alive dlts
                               // | hier: hts cum_drift drift dhts cum_alive bxy2
 
@@ -84,6 +84,8 @@ __device__ inline void load_book(const KArgs& a, int i, Book& b) {
     b.frame = bi[0 * a.n + i]; b.timestep = bi[1 * a.n + i]; b.pred_idx = bi[2 * a.n + i];
     b.clip = bi[3 * a.n + i]; b.rng_ctr = (unsigned)bi[4 * a.n + i]; b.mode = (unsigned)bi[5 * a.n + i];
     b.rng_key = (unsigned long long)(unsigned)bi[6 * a.n + i] | ((unsigned long long)(unsigned)bi[7 * a.n + i] << 32);
+    b.terrain_key = a.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS
+        ? ((unsigned long long)(unsigned)bi[11 * a.n + i] | ((unsigned long long)(unsigned)bi[12 * a.n + i] << 32)) : 0ull;
     const double* d = a.bd;
     auto D = [&](int e) { return d[(long)e * a.n + i]; };
     for (int k = 0; k < 3; k++) { b.target[k] = D(k); b.srp[k] = D(3 + k); b.robot_pos[k] = D(6 + k); b.sep[k] = D(9 + k); }
@@ -106,6 +108,10 @@ __device__ inline void store_book(const KArgs& a, int i, const Book& b) {
     int* bi = a.bi;
     bi[0 * a.n + i] = b.frame; bi[1 * a.n + i] = b.timestep; bi[2 * a.n + i] = b.pred_idx;
     bi[3 * a.n + i] = b.clip; bi[4 * a.n + i] = (int)b.rng_ctr; bi[5 * a.n + i] = (int)b.mode;
+    if (a.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS) {
+        bi[11 * a.n + i] = (int)(unsigned)(b.terrain_key & 0xffffffffull);
+        bi[12 * a.n + i] = (int)(unsigned)(b.terrain_key >> 32);
+    }
     double* d = a.bd;
     auto D = [&](int e) -> double& { return d[(long)e * a.n + i]; };
     for (int k = 0; k < 3; k++) { D(k) = b.target[k]; D(3 + k) = b.srp[k]; D(6 + k) = b.robot_pos[k]; D(9 + k) = b.sep[k]; }
@@ -150,6 +156,8 @@ template <typename T>
 __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i, T* st, Book& b, int start_frame, double reset_yaw, float* obs,
                            unsigned& ef, const T* scs = nullptr) {   // scs: the reset pose's hinge sin / cos
     const ClipDev& c = a.clips[b.clip];
+    // flat_env.reset() -> CustomScene.episode_restart: a new random terrain (humanoid.py:89-113)
+    if (a.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS) b.terrain_key = next_terrain_key(b.terrain_key, b.rng_key);
     const bool ref = !(a.reset_flags & HUM_RESET_NO_REF_POSE);                // startFromRef
     const bool init_vel = ref && !(a.reset_flags & HUM_RESET_NO_INIT_VEL);   // startFromRef and initVel (:291)
     if (ref && start_frame < 0) start_frame = draw(a, i, b, 0, c.max_frame - 5);   // :228
@@ -625,8 +633,11 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
 // Cooperative step: 16 lanes per env, EPB_ envs per block of EPB_*16 threads (one wavefront), env working
 // set in LDS.  EPB_ = 4 fills the wave; EPB_ = 2 leaves half of it idle but lets a SIMD hold two waves
 // (19.3 KB LDS per block), so one wave's LDS/memory waits overlap the other's VALU issue.
-template <typename T, int EPB_>
-__global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
+#ifndef HUM_GROUP_MIN_WAVES
+#define HUM_GROUP_MIN_WAVES 1
+#endif
+template <typename T, int EPB_, bool TERRAIN = false>
+__global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a) {
     __shared__ GroupLDS<T> sh[EPB_];
     const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
     // XCD-aware env mapping: the dispatcher deals blocks round-robin over the 8 XCDs (block b -> XCD b % 8),
@@ -664,11 +675,14 @@ __global__ void __launch_bounds__(EPB_ * GL) step_group_kernel(KArgs a) {
     const bool any_phys = __ballot(valid && !high && !skip) != 0;   // wave-uniform
     __syncthreads();
     unsigned ef = 0;
+    // the env's terrain (HUM_TERRAIN_RANDOM_BLOCKS: drawn at its last reset)
+    const unsigned long long tkey = TERRAIN && a.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid
+        ? ((unsigned long long)(unsigned)a.bi[11 * a.n + i] | ((unsigned long long)(unsigned)a.bi[12 * a.n + i] << 32)) : 0ull;
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++)
-            group_substep<T, EPB_>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_block_size(EPB_, a.P.lds_rows),
-                                   l, ef);
+            group_substep<T, EPB_, TERRAIN>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_block_size(EPB_, a.P.lds_rows),
+                                   l, ef, tkey);
     }
     // hinge sin / cos of the final physics state, one dof per lane, for calc_state's kinematics on lane 0
     T* scs = &sh[ge].x.aba.IA[0][0];

@@ -32,6 +32,11 @@ struct PhysParams {
     int self_collision;
     int joint_damping;
     int lds_rows;         // cooperative kernel: constraint rows per block kept in LDS (block row pool capacity)
+    // ground (hum_set_terrain, terrain.h): 0 = plane z = 0, 1 = shared heightfield hf, 2 = per-lane random blocks
+    int terrain;
+    const float* hf;      // terrain 1: heights [hf_w * hf_l], vertex (i, j) at hf[i + j * hf_w]
+    int hf_w, hf_l;
+    double hf_s[3], hf_o[3], hf_mid;   // mesh scale, body origin, vertical centre (min + max) / 2
 };
 
 constexpr int NV = 6 + NDOF;

@@ -15,6 +15,7 @@
 //   PGS             rows in Bullet order; J.nu over the 16 lanes by DPP row_ror reductions
 #pragma once
 #include "physics.h"
+#include "terrain.h"
 
 namespace hk {
 
@@ -974,9 +975,10 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
 
 // ------------------------------------------------------------------------- one cooperative substep
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
-template <typename T, int EPB_>
+template <typename T, int EPB_, bool TERRAIN = false>   // TERRAIN: heightfield ground (hum_set_terrain)
 __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>* shb, const int ge,
-                                                             T* gblock, const int l, unsigned& ef) {
+                                                             T* gblock, const int l, unsigned& ef,
+                                                             unsigned long long tkey) {   // tkey: terrain 2
     GroupLDS<T>& S = shb[ge];
     const ModelTab<T>& M = tab<T>();
     const T dt = (T)P.dt;
@@ -1250,22 +1252,45 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         }
         nc += __popcll(bm);
     };
+    if constexpr (!TERRAIN) {
 #pragma unroll
-    for (int r = 0; r < CC_GROUND; r++) {   // sphere / capsule end vs plane (cheap, exact)
-        const int gd = lane16(lc, CDESC.g[r][0], CDESC.g[r][1], CDESC.g[r][2], CDESC.g[r][3]);
-        bool hit = false;
-        int ba = 0;
-        T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
-        if (gd != 0xffff) {
-            const int ga = gd & 31, e = (gd >> 5) & 1;
-            const T gr = geom_r_l<T>(ga);
-            const T* p = C.gp[ga][e];
-            d = basez + p[2] - gr;
-            hit = d < (T)P.contact_thresh;
-            ba = gd >> 6;
-            pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - gr;
+        for (int r = 0; r < CC_GROUND; r++) {   // sphere / capsule end vs plane (cheap, exact)
+            const int gd = lane16(lc, CDESC.g[r][0], CDESC.g[r][1], CDESC.g[r][2], CDESC.g[r][3]);
+            bool hit = false;
+            int ba = 0;
+            T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
+            if (gd != 0xffff) {
+                const int ga = gd & 31, e = (gd >> 5) & 1;
+                const T gr = geom_r_l<T>(ga);
+                const T* p = C.gp[ga][e];
+                d = basez + p[2] - gr;
+                hit = d < (T)P.contact_thresh;
+                ba = gd >> 6;
+                pa[0] = p[0]; pa[1] = p[1]; pa[2] = p[2] - gr;
+            }
+            emit(hit, ba, -1, pa, pa, n, d);
         }
-        emit(hit, ba, -1, pa, pa, n, d);
+    } else {
+        // heightfield (terrain.h): the same candidates against the closest point of the terrain surface (a
+        // separate kernel instantiation, so the plane kernel carries none of this code)
+#pragma unroll 1
+        for (int r = 0; r < CC_GROUND; r++) {
+            const int gd = lane16(lc, CDESC.g[r][0], CDESC.g[r][1], CDESC.g[r][2], CDESC.g[r][3]);
+            bool hit = false;
+            int ba = 0;
+            T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
+            if (gd != 0xffff) {
+                const int ga = gd & 31, e = (gd >> 5) & 1;
+                const T gr = geom_r_l<T>(ga);
+                const T* p = C.gp[ga][e];
+                const T cw[3] = {S.st[0] + p[0], S.st[1] + p[1], basez + p[2]};
+                hit = terrain_contact<T>(P, tkey, cw, gr, n, d);
+                ba = gd >> 6;
+#pragma unroll
+                for (int i = 0; i < 3; i++) pa[i] = p[i] - gr * n[i];
+            }
+            emit(hit, ba, -1, pa, pa, n, d);
+        }
     }
     if (P.self_collision) {
         // broad phase: bounding spheres about the segment midpoints (conservative margin), survivors listed

@@ -8,7 +8,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
-HUM_ABI_VERSION = 5   # include/humanoid_env.h
+HUM_ABI_VERSION = 6   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
@@ -18,6 +18,7 @@ HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW, HUM_E
 HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
 HUM_RESET_NO_REF_POSE, HUM_RESET_NO_INIT_VEL = 1, 2
 HUM_MAX_CONTACTS = 95
+HUM_TERRAIN_PLANE, HUM_TERRAIN_HEIGHTFIELD, HUM_TERRAIN_RANDOM_BLOCKS = 0, 1, 2
 
 # bookkeeping layout (HUM_BK_*)
 BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, target=4, starting_robot_pos=7,
@@ -26,7 +27,9 @@ BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, targe
           aliveReward=25, delta_lowTargetScore=26, clip=27, mode=28, rng_key_lo=29, rng_key_hi=30,
           # hierarchical env (hier_env.py)
           steps_remaining_at_level=31, num_high_level_steps=32, expect_high=33, highTargetScore=34,
-          cumulative_driftScore=35, driftScore=36, delta_highTargetScore=37, cumulative_aliveReward=38, body_xy=39)
+          cumulative_driftScore=35, driftScore=36, delta_highTargetScore=37, cumulative_aliveReward=38, body_xy=39,
+          # HUM_TERRAIN_RANDOM_BLOCKS: the lane's current terrain key
+          terrain_key_lo=41, terrain_key_hi=42)
 AUX = ["deltaJoints", "deltaEndPoints", "lowTargetScore", "deltaVelJoints", "bodyPostureScore", "highTargetScore",
        "driftScore", "baseReward", "aliveReward", "electricityScore", "jointLimitScore", "dist_from_origin",
        "endPointScore", "endPointScoreExp", "robot_pos_x", "robot_pos_y", "robot_pos_z"]
@@ -37,7 +40,7 @@ EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_creat
            "hum_step_graph", "hum_get_aux", "hum_get_state", "hum_set_state", "hum_get_parts",
            "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step",
            "hum_reset_ex", "hum_hier_reset_ex", "hum_clip_csv_sizes", "hum_clip_csv_parse", "hum_load_clip_csv",
-           "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout"]
+           "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout", "hum_set_terrain"]
 
 
 class HumConfig(ctypes.Structure):
@@ -82,6 +85,7 @@ def lib():
     L.hum_set_lane_clips.argtypes = [vp, vp]
     L.hum_set_lane_modes.argtypes = [vp, vp]
     L.hum_set_predefined_targets.argtypes = [vp, dp, i32]
+    L.hum_set_terrain.argtypes = [vp, i32, vp, i32, i32, dp, dp]
     L.hum_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hum_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.hum_clip_csv_sizes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]

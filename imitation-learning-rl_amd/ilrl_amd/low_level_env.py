@@ -100,8 +100,6 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
 
     def __init__(self, reference_name="motion08_03", useCustomEnv=False, customRobot=None, seed=None, device=0,
                  precision="fp32", lane_offset=0, **physics):
-        if useCustomEnv:
-            raise NotImplementedError("useCustomEnv (heightfield terrain, humanoid.py:68-188) is out of scope")
         if seed is None:   # the reference's unseeded default_rng() (:84): a fresh stream per env
             seed = secrets.randbits(63)
         self.__dict__["_v"] = HumanoidVecEnv(1, clips=(reference_name,), seed=seed, device=device,
@@ -116,6 +114,10 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
         self.skipFrame = 2
         self.targetLen = 5
         self.max_frame = self._v.clips[0].max_frame
+        self.useCustomEnv = bool(useCustomEnv)
+        if self.useCustomEnv:   # :41-42 CustomHumanoid: CustomScene's random heightfield instead of the plane
+            self._v.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
+            self.__dict__["flat_env"] = _CustomEnvView(self._v)
 
     def __setattr__(self, name, value):
         if name == "usePredefinedTarget":
@@ -149,12 +151,20 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
         self.__dict__["_cache"] = None
         return t[0].double().cpu().numpy()
 
+    def _scene_restart(self):
+        # flat_env.reset() -> CustomScene.episode_restart: a fresh random terrain, whatever replaceHeightfieldData
+        # installed during the previous episode (humanoid.py:89-113)
+        if self.useCustomEnv and self._v.terrain != N.HUM_TERRAIN_RANDOM_BLOCKS:
+            self._v.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
+
     def reset(self, resetYaw=0):                                        # low_level_env.py:224-232
+        self._scene_restart()
         return self._obs(self._v.reset(reset_yaw=float(resetYaw)))
 
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :247-305
         if startFromRef and not 0 <= int(startFrame) < self.max_frame + 1:   # DataFrame.iloc (:208) raises
             raise IndexError("single positional indexer is out-of-bounds (startFrame=%d)" % int(startFrame))
+        self._scene_restart()
         return self._obs(self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw),
                                        start_from_ref=startFromRef, init_vel=initVel))
 
@@ -173,6 +183,31 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
 
     def render(self, mode="human"):
         raise NotImplementedError("rendering is out of scope (env_vis_low.py)")
+
+
+class _CustomSceneView:
+    """flat_env.stadium_scene of a useCustomEnv env (humanoid.py:68-86 CustomScene): replaceHeightfieldData(d)
+    installs a 256 x 256 heightfield (d[i + j*256], i along x) at z 0.25 until the next reset, as in
+    env_vis_low.py:155-171."""
+    numHeightfieldRows = 256
+    numHeightfieldColumns = 256
+
+    def __init__(self, venv):
+        self._venv = venv
+        self.heightfieldData = [0] * (self.numHeightfieldRows * self.numHeightfieldColumns)
+
+    def replaceHeightfieldData(self, newData):
+        self.heightfieldData = list(newData)
+        self._venv.set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=np.asarray(self.heightfieldData, dtype=np.float32),
+                               w=self.numHeightfieldRows, l=self.numHeightfieldColumns, scale=(1.0, 1.0, 1.0),
+                               origin=(0.0, 0.0, 0.25))
+
+
+class _CustomEnvView:
+    """flat_env of a useCustomEnv env: the CustomHumanoid scene handle (stadium_scene)."""
+
+    def __init__(self, venv):
+        self.stadium_scene = _CustomSceneView(venv)
 
 
 # RewardLogCallback attributes (custom_callback.py:43-80) served from the device aux row of ONE lane

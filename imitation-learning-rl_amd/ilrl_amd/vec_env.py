@@ -25,6 +25,7 @@ class HumanoidVecEnv:
 
     def __init__(self, n, clips=("motion02_04",), clip_of_lane=None, seed=0, device=0, lane_offset=0,
                  precision="fp32", block_size=64, **physics):
+        self.terrain = N.HUM_TERRAIN_PLANE
         import torch
         if not torch.cuda.is_available():
             raise N.NativeError("HumanoidVecEnv needs a HIP device (no CPU fallback by design)")
@@ -78,6 +79,22 @@ class HumanoidVecEnv:
         if predefined is not None:
             m |= np.where(np.broadcast_to(predefined, self.n), N.HUM_MODE_PREDEFINED, 0).astype(np.uint32)
         N.check(N.lib().hum_set_lane_modes(self.h, m.ctypes.data_as(ctypes.c_void_p)), "hum_set_lane_modes")
+
+    def set_terrain(self, mode, heights=None, w=256, l=256, scale=(1.0, 1.0, 1.0), origin=(0.0, 0.0, 0.25)):
+        """Ground of every lane (hum_set_terrain): N.HUM_TERRAIN_PLANE, N.HUM_TERRAIN_HEIGHTFIELD (heights [w*l],
+        vertex (i, j) = heights[i + j*w], CustomScene.replaceHeightfieldData's layout) or
+        N.HUM_TERRAIN_RANDOM_BLOCKS (LowLevelHumanoidEnv(useCustomEnv=True): a new CustomScene terrain per lane at
+        every reset)."""
+        h = None
+        if mode == N.HUM_TERRAIN_HEIGHTFIELD:
+            h = np.ascontiguousarray(heights, dtype=np.float32).reshape(-1)
+            if h.size != w * l:
+                raise ValueError("heights: %d values for a %d x %d heightfield" % (h.size, w, l))
+        sc = np.ascontiguousarray(scale, dtype=np.float64)
+        org = np.ascontiguousarray(origin, dtype=np.float64)
+        N.check(N.lib().hum_set_terrain(self.h, int(mode), h.ctypes.data if h is not None else None, int(w), int(l),
+                                        _dp(sc), _dp(org)), "hum_set_terrain")
+        self.terrain = int(mode)
 
     def set_predefined_targets(self, xyz):
         xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)

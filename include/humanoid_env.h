@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 5
+#define HUM_ABI_VERSION 6
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -87,8 +87,16 @@ enum {
        cumulative_aliveReward, flat_env.robot.body_xyz[0:2] of the last calc_state */
     HUM_BK_LEVEL_REMAINING = 31, HUM_BK_NUM_HIGH_STEPS = 32, HUM_BK_EXPECT_HIGH = 33, HUM_BK_HIGH_TARGET_SCORE = 34,
     HUM_BK_CUM_DRIFT = 35, HUM_BK_DRIFT = 36, HUM_BK_DELTA_HIGH_TARGET = 37, HUM_BK_CUM_ALIVE = 38,
-    HUM_BK_BODY_XY /* 2 */ = 39
+    HUM_BK_BODY_XY /* 2 */ = 39,
+    /* HUM_TERRAIN_RANDOM_BLOCKS: the 64-bit key of the lane's current terrain (two u32 halves), redrawn at every
+       reset as CustomScene.episode_restart regenerates the heightfield (humanoid.py:89-113) */
+    HUM_BK_TERRAIN_KEY_LO = 41, HUM_BK_TERRAIN_KEY_HI = 42
 };
+
+/* hum_set_terrain modes: the ground the contacts are generated against */
+#define HUM_TERRAIN_PLANE 0          /* HumanoidBulletEnv's StadiumScene plane z = 0 (default; every config) */
+#define HUM_TERRAIN_HEIGHTFIELD 1    /* one heightfield shared by all lanes (CustomScene.replaceHeightfieldData) */
+#define HUM_TERRAIN_RANDOM_BLOCKS 2  /* LowLevelHumanoidEnv(useCustomEnv=True): per-lane CustomScene terrain */
 
 /* hum_hier_step per-lane agent mask (which entries of the reference's obs/rew dicts are present) */
 #define HUM_AGENT_HIGH 1u   /* "high_level_agent" obs + reward */
@@ -178,6 +186,25 @@ int hum_set_clip(hum_env* env, int32_t clip_id, const double* pos, int32_t n_pos
 int hum_clip_csv_sizes(const char* dir, const char* name, int32_t* sizes4);
 int hum_clip_csv_parse(const char* dir, const char* name, double* pos, double* vel, double* rel, double* ep);
 int hum_load_clip_csv(hum_env* env, int32_t clip_id, const char* dir, const char* name);
+
+/* Ground of the handle's lanes (LowLevelHumanoidEnv(useCustomEnv=True) -> humanoid.py:68-144 CustomScene, a
+ * pybullet GEOM_HEIGHTFIELD body instead of the plane).  Cooperative kernel (hum_config.kernel = 1), low-level
+ * env (hier = 0) only.
+ *   HUM_TERRAIN_PLANE: the plane z = 0 (default).
+ *   HUM_TERRAIN_HEIGHTFIELD: heights[w * l] float32, vertex (i, j) = heights[i + j * w] (pybullet heightfieldData
+ *     order: i along x), mesh scale scale3, body at origin3 (identity orientation); Bullet's btHeightfieldTerrainShape
+ *     geometry: vertex (i, j) at origin + scale * (i - (w-1)/2, j - (l-1)/2, h - (min + max)/2), two triangles per
+ *     cell split by diamond subdivision.  CustomScene.replaceHeightfieldData(d) = (d, 256, 256, {1,1,1}, {0,0,0.25}).
+ *     Requires scale x, y >= 0.25 (a contact candidate reaches at most 2 x 2 cells).
+ *   HUM_TERRAIN_RANDOM_BLOCKS: CustomScene.episode_restart's terrain per lane, regenerated at every reset: 256 x 256
+ *     vertices in 2 x 2 blocks of height random.uniform(0, 0.05) * 10, the four centre blocks 0, body at
+ *     (0, 0, 0.25); block heights are counter-based draws from the lane's terrain key (HUM_BK_TERRAIN_KEY_*),
+ *     and the vertical centring uses the distribution's range (0 + 0.5) / 2.  heights / w / l /
+ *     scale3 / origin3 are ignored (may be NULL).
+ * Contacts: every sphere / capsule-end ground candidate against the closest point of the terrain surface (the
+ * cells within reach).  A captured step graph is recaptured. */
+int hum_set_terrain(hum_env* env, int32_t mode, const float* heights, int32_t w, int32_t l, const double* scale3,
+                    const double* origin3);
 
 /* clip id per lane (host array of n_lanes); default all 0 */
 int hum_set_lane_clips(hum_env* env, const int32_t* clip_of_lane);

@@ -64,7 +64,57 @@ class OmParams(ctypes.Structure):
                 ("lin_damp", ctypes.c_double), ("ang_damp", ctypes.c_double),
                 ("limit_max_impulse", ctypes.c_double), ("max_contacts", ctypes.c_int),
                 ("self_collision", ctypes.c_int), ("joint_damping", ctypes.c_int),
-                ("max_coord_vel", ctypes.c_double)]
+                ("max_coord_vel", ctypes.c_double),
+                # ground: 0 plane, 1 heightfield hf, 2 CustomScene random blocks (physics_oracle.c terrain_contact)
+                ("terrain", ctypes.c_int), ("hf", ctypes.c_void_p), ("hf_w", ctypes.c_int), ("hf_l", ctypes.c_int),
+                ("hf_s", ctypes.c_double * 3), ("hf_o", ctypes.c_double * 3), ("hf_mid", ctypes.c_double),
+                ("terrain_key", ctypes.c_uint64)]
+
+
+TERRAIN_PLANE, TERRAIN_HEIGHTFIELD, TERRAIN_RANDOM_BLOCKS = 0, 1, 2
+TERRAIN_SALT = 0x2545F4914F6CDD1D
+
+
+class Terrain:
+    """Ground of an oracle env (hum_set_terrain restated): TERRAIN_HEIGHTFIELD with heights [w*l] (vertex (i, j)
+    at heights[i + j*w]), mesh scale and body origin as CustomScene / pybullet take them; TERRAIN_RANDOM_BLOCKS =
+    CustomScene.episode_restart's terrain (humanoid.py:89-113) regenerated at every reset from a per-env key."""
+
+    def __init__(self, mode, heights=None, w=256, l=256, scale=(1.0, 1.0, 1.0), origin=(0.0, 0.0, 0.25)):
+        self.mode = mode
+        self.w, self.l = w, l
+        self.scale, self.origin = tuple(scale), tuple(origin)
+        self.heights = None
+        self.mid = 0.25   # random blocks: the range midpoint (0 + 0.5) / 2
+        if mode == TERRAIN_HEIGHTFIELD:
+            self.heights = np.ascontiguousarray(heights, dtype=np.float32).reshape(-1)
+            assert self.heights.size == w * l
+            self.mid = 0.5 * (float(self.heights.min()) + float(self.heights.max()))   # btHeightfieldTerrainShape
+
+    def apply(self, P, key=0):
+        P.terrain = self.mode
+        P.hf = self.heights.ctypes.data if self.heights is not None else None
+        P.hf_w, P.hf_l = self.w, self.l
+        for k in range(3):
+            P.hf_s[k] = self.scale[k]
+            P.hf_o[k] = self.origin[k]
+        P.hf_mid = self.mid
+        P.terrain_key = key
+        return P
+
+
+def next_terrain_key(prev, rng_key):
+    """The lane's terrain after a reset (CustomScene.episode_restart): chained from the previous terrain key."""
+    return splitmix64((prev ^ rng_key ^ TERRAIN_SALT) & M64)
+
+
+def random_block_height(key, bi, bj):
+    """humanoid.py:96-101: random.uniform(0, 0.05) * 10 per 2x2 block (counter-based 53-bit uniform), the four
+    centre blocks 0; float32 as pybullet stores heightfield data."""
+    if bi in (63, 64) and bj in (63, 64):
+        return np.float32(0.0)
+    u = (splitmix64((key + bi + 128 * bj) & M64) >> 11) * (1.0 / 9007199254740992.0)
+    return np.float32((0.05 * u) * 10.0)
 
 
 _lib = None
@@ -266,9 +316,11 @@ def get_joint_pos(clip, row, joint):
 class OracleLowLevelEnv:
     """Single-lane restatement of LowLevelHumanoidEnv (low_level_env.py:36-526)."""
 
-    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=DEFAULT_NUMPY):
+    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=DEFAULT_NUMPY, terrain=None):
         self.clip = clip
         self.params = params
+        self.terrain = terrain          # None / Terrain (LowLevelHumanoidEnv(useCustomEnv=True): CustomScene)
+        self.terrain_key = 0
         self.numpy_semantics = numpy_semantics
         self.cur_timestep = 0
         self.max_timestep = 3000                                    # :73
@@ -337,7 +389,19 @@ class OracleLowLevelEnv:
             setattr(o, k, float(book[bk[k]]))
         key = int(book[bk["rng_key_lo"]]) | (int(book[bk["rng_key_hi"]]) << 32)
         o.rng = LaneRNG(key=key, counter=int(book[bk["rng_counter"]]))
+        if "terrain_key_lo" in bk:
+            o.terrain_key = int(book[bk["terrain_key_lo"]]) | (int(book[bk["terrain_key_hi"]]) << 32)
         return o
+
+    def _phys_params(self):
+        if self.terrain is None or self.terrain.mode == TERRAIN_PLANE:
+            return self.params
+        P = OmParams()
+        if self.params is not None:
+            ctypes.memmove(ctypes.byref(P), ctypes.byref(self.params), ctypes.sizeof(OmParams))
+        else:
+            lib().om_default_params(ctypes.byref(P))
+        return self.terrain.apply(P, self.terrain_key)
 
     # -- physics-facing helpers (stand in for flat_env / robot) ----------------------------------------
     def _calc_state(self):
@@ -375,6 +439,8 @@ class OracleLowLevelEnv:
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):  # :247-305
         # flat_env.reset(): restoreState -> zero velocities; robot_specific_reset re-randomises joints
         # (all 17 are overwritten below when startFromRef)
+        if self.terrain is not None and self.terrain.mode == TERRAIN_RANDOM_BLOCKS:   # CustomScene.episode_restart
+            self.terrain_key = next_terrain_key(self.terrain_key, self.rng.key)
         self.state[:] = 0
         self.state[6] = 1.0
         if not startFromRef:
@@ -529,7 +595,7 @@ class OracleLowLevelEnv:
     def step(self, action, debug=False, physics=True):              # :475-526
         action = np.asarray(action, dtype=np.float32)
         if physics:
-            self.state = phys_step(self.state, motor_torques(action, self.numpy_semantics), self.params)
+            self.state = phys_step(self.state, motor_torques(action, self.numpy_semantics), self._phys_params())
         self.cur_obs = self._calc_state()
         self.robot_pos[0] = self.body_xyz[0]
         self.robot_pos[1] = self.body_xyz[1]

@@ -53,6 +53,13 @@ typedef struct {
     int self_collision;
     int joint_damping;      /* 0: ignore MJCF joint damping, 1: implicit per substep (default) */
     double max_coord_vel;   /* btMultiBody::m_maxCoordinateVelocity clamp in applyDeltaVeeMultiDof */
+    /* ground (hum_set_terrain): 0 = plane z = 0, 1 = heightfield hf, 2 = CustomScene random blocks from
+       terrain_key (humanoid.py:68-144) */
+    int terrain;
+    const float* hf;        /* terrain 1: heights, vertex (i, j) = hf[i + j * hf_w] */
+    int hf_w, hf_l;
+    double hf_s[3], hf_o[3], hf_mid;
+    unsigned long long terrain_key;
 } om_params;
 
 /* ------------------------------------------------------------------------- small linear algebra */
@@ -453,6 +460,114 @@ static void seg_seg(const double* p1, const double* q1, const double* p2, const 
     for (int i = 0; i < 3; i++) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
 }
 
+/* --------------------------------------------------------------------------- heightfield ground
+ * Bullet btHeightfieldTerrainShape (upAxis z, float data, diamond subdivision): vertex (i, j) at
+ * origin + scale * (i - (w-1)/2, j - (l-1)/2, h - mid); cell (i, j) split along (i,j)-(i+1,j+1) when i + j is
+ * even, along (i+1,j)-(i,j+1) otherwise.  A ground candidate sphere touches the closest point of the surface
+ * over the triangles of the cells within reach; a centre below the plane of the triangle under it takes that
+ * triangle's upward normal. */
+static unsigned long long sm64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static float block_height(unsigned long long key, int bi, int bj) {   /* humanoid.py:94-111 */
+    if ((bi == 63 || bi == 64) && (bj == 63 || bj == 64)) return 0.f;
+    double u = (double)(sm64(key + (unsigned long long)(bi + 128 * bj)) >> 11) * (1.0 / 9007199254740992.0);
+    return (float)((0.05 * u) * 10.0);
+}
+static void hf_vertex(const om_params* P, int i, int j, double* v) {
+    float h = P->terrain == 1 ? P->hf[i + j * P->hf_w] : block_height(P->terrain_key, i >> 1, j >> 1);
+    v[0] = ((double)i - 0.5 * (P->hf_w - 1)) * P->hf_s[0] + P->hf_o[0];
+    v[1] = ((double)j - 0.5 * (P->hf_l - 1)) * P->hf_s[1] + P->hf_o[1];
+    v[2] = ((double)h - P->hf_mid) * P->hf_s[2] + P->hf_o[2];
+}
+static void tri_corners(int ci, int cj, int t, int* di, int* dj) {
+    static const int A[2][2][6] = {{{0, 0, 1, 0, 1, 1}, {0, 1, 1, 0, 1, 0}}, {{0, 0, 1, 0, 1, 0}, {1, 0, 1, 0, 1, 1}}};
+    const int* o = A[((ci + cj) & 1) ? 1 : 0][t];
+    for (int k = 0; k < 3; k++) { di[k] = o[k]; dj[k] = o[3 + k]; }
+}
+/* closest point of triangle abc to p (Ericson 5.1.5) */
+static void closest_tri(const double* p, const double* a, const double* b, const double* c, double* q) {
+    double ab[3], ac[3], ap[3], bp[3], cp[3];
+    for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ap[k] = p[k] - a[k]; }
+    double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+    if (d1 <= 0 && d2 <= 0) { memcpy(q, a, 3 * sizeof(double)); return; }
+    for (int k = 0; k < 3; k++) bp[k] = p[k] - b[k];
+    double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+    if (d3 >= 0 && d4 <= d3) { memcpy(q, b, 3 * sizeof(double)); return; }
+    double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0 && d1 >= 0 && d3 <= 0) { double t = d1 / (d1 - d3); for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k]; return; }
+    for (int k = 0; k < 3; k++) cp[k] = p[k] - c[k];
+    double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+    if (d6 >= 0 && d5 <= d6) { memcpy(q, c, 3 * sizeof(double)); return; }
+    double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0 && d2 >= 0 && d6 <= 0) { double t = d2 / (d2 - d6); for (int k = 0; k < 3; k++) q[k] = a[k] + t * ac[k]; return; }
+    double va = d3 * d6 - d5 * d4;
+    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+        double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        for (int k = 0; k < 3; k++) q[k] = b[k] + t * (c[k] - b[k]);
+        return;
+    }
+    double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
+    for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
+}
+static int terrain_contact(const om_params* P, const double* c, double r, double* n, double* d) {
+    double u = (c[0] - P->hf_o[0]) / P->hf_s[0] + 0.5 * (P->hf_w - 1);
+    double v = (c[1] - P->hf_o[1]) / P->hf_s[1] + 0.5 * (P->hf_l - 1);
+    if (!(u > -2 && u < P->hf_w + 1 && v > -2 && v < P->hf_l + 1)) return 0;
+    double reach = r + P->contact_thresh;
+    int i0 = (int)floor(u - reach / P->hf_s[0]), i1 = (int)floor(u + reach / P->hf_s[0]);
+    int j0 = (int)floor(v - reach / P->hf_s[1]), j1 = (int)floor(v + reach / P->hf_s[1]);
+    if (i0 < 0) i0 = 0;
+    if (j0 < 0) j0 = 0;
+    if (i1 > P->hf_w - 2) i1 = P->hf_w - 2;
+    if (j1 > P->hf_l - 2) j1 = P->hf_l - 2;
+    if (i0 > i1 || j0 > j1) return 0;
+    double best = -1, q[3] = {0, 0, 0};
+    for (int cj = j0; cj <= j1; cj++)
+        for (int ci = i0; ci <= i1; ci++)
+            for (int t = 0; t < 2; t++) {
+                int di[3], dj[3];
+                double va[3], vb[3], vc[3], qq[3], dv[3];
+                tri_corners(ci, cj, t, di, dj);
+                hf_vertex(P, ci + di[0], cj + dj[0], va);
+                hf_vertex(P, ci + di[1], cj + dj[1], vb);
+                hf_vertex(P, ci + di[2], cj + dj[2], vc);
+                closest_tri(c, va, vb, vc, qq);
+                for (int k = 0; k < 3; k++) dv[k] = c[k] - qq[k];
+                double d2 = dot3(dv, dv);
+                if (best < 0 || d2 < best) { best = d2; memcpy(q, qq, sizeof q); }
+            }
+    double nf[3] = {0, 0, 1}, sd = 1;
+    int fi = (int)floor(u), fj = (int)floor(v);
+    if (fi >= 0 && fi <= P->hf_w - 2 && fj >= 0 && fj <= P->hf_l - 2) {
+        double fa = u - fi, fb = v - fj;
+        int t = !((fi + fj) & 1) ? (fb >= fa ? 0 : 1) : (fa + fb <= 1 ? 0 : 1);
+        int di[3], dj[3];
+        double va[3], vb[3], vc[3], e1[3], e2[3], ap[3];
+        tri_corners(fi, fj, t, di, dj);
+        hf_vertex(P, fi + di[0], fj + dj[0], va);
+        hf_vertex(P, fi + di[1], fj + dj[1], vb);
+        hf_vertex(P, fi + di[2], fj + dj[2], vc);
+        for (int k = 0; k < 3; k++) { e1[k] = vb[k] - va[k]; e2[k] = vc[k] - va[k]; ap[k] = c[k] - va[k]; }
+        cross(e1, e2, nf);
+        double il = (nf[2] < 0 ? -1.0 : 1.0) / norm3(nf);
+        for (int k = 0; k < 3; k++) nf[k] *= il;
+        sd = dot3(ap, nf);
+    }
+    if (sd < 0) {
+        memcpy(n, nf, 3 * sizeof(double));
+        *d = sd - r;
+    } else {
+        double dist = sqrt(best);
+        if (dist <= 1e-9) { memcpy(n, nf, 3 * sizeof(double)); *d = -r; }
+        else { for (int k = 0; k < 3; k++) n[k] = (c[k] - q[k]) / dist; *d = dist - r; }
+    }
+    return *d < P->contact_thresh;
+}
+
 static int collide(const om_params* P, const om_kin* K, om_contact* C) {
     int nc = 0;
     double gp1[OM_NG][3], gp2[OM_NG][3];
@@ -464,6 +579,20 @@ static int collide(const om_params* P, const om_kin* K, om_contact* C) {
         int ne = om_gtype[g] == 0 ? 1 : 2;
         for (int e = 0; e < ne; e++) {
             const double* p = e == 0 ? gp1[g] : gp2[g];
+            if (P->terrain) {   /* heightfield ground */
+                double n[3], d;
+                if (terrain_contact(P, p, om_gr[g], n, &d) && nc < P->max_contacts) {
+                    om_contact* c = &C[nc++];
+                    c->la = om_glink[g]; c->lb = -1;
+                    for (int i = 0; i < 3; i++) {
+                        c->n[i] = n[i];
+                        c->pa[i] = p[i] - om_gr[g] * n[i];
+                        c->pb[i] = c->pa[i] - d * n[i];
+                    }
+                    c->d = d; c->mu = P->mu_ground;
+                }
+                continue;
+            }
             double d = p[2] - om_gr[g];
             if (d < P->contact_thresh && nc < P->max_contacts) {
                 om_contact* c = &C[nc++];
@@ -681,6 +810,13 @@ void om_default_params(om_params* P) {
     P->self_collision = 1;
     P->joint_damping = 1;
     P->max_coord_vel = 100.0;
+    P->terrain = 0;
+    P->hf = 0;
+    P->hf_w = P->hf_l = 256;
+    for (int k = 0; k < 3; k++) { P->hf_s[k] = 1.0; P->hf_o[k] = 0.0; }
+    P->hf_o[2] = 0.25;
+    P->hf_mid = 0.25;
+    P->terrain_key = 0;
 }
 
 /* one env step of physics: state (47) in place; tau_motor[17] in dof order (already 0.41*power*clip(a)). */
@@ -706,3 +842,9 @@ void om_link_frames(const double* st, double* R, double* x) {
     memcpy(x, K.x, sizeof K.x);
 }
 int om_nv(void) { return NV; }
+
+/* one ground candidate (sphere centre c, radius r) against the heightfield ground: 1 with normal n and signed
+   distance d when in contact range (tests) */
+int om_terrain_contact(const om_params* P, const double* c, double r, double* n, double* d) {
+    return terrain_contact(P, c, r, n, d);
+}

@@ -1,0 +1,195 @@
+"""GPU parity of the heightfield ground (hum_set_terrain; LowLevelHumanoidEnv(useCustomEnv=True) ->
+CustomScene, /root/reference/humanoid.py:68-144) against the oracle's restatement (oracle/physics_oracle.c
+terrain_contact, oracle.Terrain).
+
+* HUM_TERRAIN_RANDOM_BLOCKS: lanes placed over random 2 x 2-block terrain (heights 0..0.5 m), one step from the
+  injected state vs the oracle with the lane's terrain key; then 40 auto-reset steps (new terrain per reset)
+  and the same one-step comparison on every sampled lane.
+* HUM_TERRAIN_HEIGHTFIELD: env_vis_low.py:155-164's ramp ("tanjakan") installed with replaceHeightfieldData's
+  layout, lanes on and around the ramp.
+* a flat heightfield at z = 0 steps like the plane; the single-env useCustomEnv view.
+
+Tolerances as tests/test_gpu_scale.py: fp64 kernel state 1e-6 (exact formulations), obs / reward 1e-5; fp32
+kernel vs the fp64 oracle over one step: FP32_BOUND; frame / timestep / RNG counter / terrain key exact.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from oracle_inject import BK, oracle_from_lane
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from ilrl_amd import _native as N  # noqa: E402
+from ilrl_amd.clips import load_clip  # noqa: E402
+from ilrl_amd.low_level_env import LowLevelHumanoidEnv  # noqa: E402
+from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
+from test_gpu_scale import FP32_BOUND  # noqa: E402
+
+CLIP = "motion08_03"
+
+
+def ramp_heights():
+    """env_vis_low.py:157-163: blocks i 63..67, j 58..69 at (i - 63) / 10, the rest 0 (vertex (x, y) at
+    data[x + y * 256])."""
+    d = np.zeros(256 * 256, dtype=np.float32)
+    for j in range(63 - 5, 64 + 5 + 1):
+        for i in range(63, 68):
+            for di in (0, 1):
+                for dj in (0, 1):
+                    d[2 * i + di + (2 * j + dj) * 256] = (i - 63) / 10
+    return d
+
+
+def _terrain_height(terrain, key, x, y):
+    """highest world z of the terrain cell under (x, y) (to lift an injected pose clear of the ground)."""
+    i, j = int(np.floor(x + 127.5)), int(np.floor(y + 127.5))
+    hs = []
+    for di in (0, 1):
+        for dj in (0, 1):
+            if terrain.mode == O.TERRAIN_RANDOM_BLOCKS:
+                h = float(O.random_block_height(key, (i + di) >> 1, (j + dj) >> 1))
+            else:
+                h = float(terrain.heights[(i + di) + (j + dj) * 256])
+            hs.append((h - terrain.mid) * terrain.scale[2] + terrain.origin[2])
+    return max(hs)
+
+
+def _place(env, terrain, rng, xy_range):
+    """move every lane's reset pose to a random (x, y) and lift it by the terrain height there."""
+    phys, book = env.get_state()
+    for k in range(env.n):
+        key = int(book[k, BK["terrain_key_lo"]]) | (int(book[k, BK["terrain_key_hi"]]) << 32)
+        x, y = rng.uniform(xy_range[0], xy_range[1]), rng.uniform(xy_range[2], xy_range[3])
+        phys[k, 0] += x
+        phys[k, 1] += y
+        phys[k, 2] += _terrain_height(terrain, key, x, y) + 0.01
+        phys[k, 7:13] += rng.uniform(-0.5, 0.5, 6)
+    env.set_state(phys, book)
+
+
+def _one_step_vs_oracle(env, terrain, a, clip):
+    phys, book = env.get_state()
+    obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
+    phys2, book2 = env.get_state()
+    res = {"state": [], "obs": [], "rew": [], "done": 0, "exact": True, "tilted": 0}
+    for i in range(env.n):
+        o = oracle_from_lane(clip, phys[i], book[i])
+        o.terrain = terrain
+        c = O.contacts(phys[i], terrain.apply(O.default_params(), o.terrain_key))
+        g = c[c[:, 1] < 0]
+        res["tilted"] += int((g[:, 9] < 0.999).sum()) if len(g) else 0
+        ro, rr, rd, _ = o.step(a[i])
+        res["state"].append(np.abs(phys2[i] - o.state).max())
+        res["obs"].append(np.abs(obs[i] - ro).max())
+        res["rew"].append(abs(float(rew[i]) - rr))
+        res["done"] += int(bool(done[i]) != rd)
+        res["exact"] &= int(frame[i]) == o.frame and int(book2[i, BK["rng_counter"]]) == o.rng.counter
+    return {k: (np.array(v) if isinstance(v, list) else v) for k, v in res.items()}
+
+
+# fp32 over terrain: the terrain is fixed in world coordinates, so (unlike the plane) contact geometry sees the
+# float32 rounding of the absolute base position: ulp(25 m) = 1.9e-6 m against 1.2e-7 m at 1 m.  Bound for bodies
+# up to 25 m from the origin: FP32_BOUND scaled by that ratio (measured maxima in the test output)
+FP32_TERRAIN_BOUND = {"obs_max": 16 * FP32_BOUND["obs_max"], "reward_max": 16 * FP32_BOUND["reward_max"]}
+
+
+def _check(res, precision):
+    print("%s: state max %.3g obs max %.3g reward max %.3g done mismatches %d" % (
+        precision, res["state"].max(), res["obs"].max(), res["rew"].max(), res["done"]))
+    assert res["exact"]
+    if precision == "fp64":
+        assert res["state"].max() < 1e-6, res["state"].max()
+        assert res["obs"].max() < 1e-5 and res["rew"].max() < 1e-5
+        assert res["done"] == 0
+    else:
+        assert res["obs"].max() <= FP32_TERRAIN_BOUND["obs_max"], res["obs"].max()
+        assert res["rew"].max() <= FP32_TERRAIN_BOUND["reward_max"], res["rew"].max()
+        assert res["done"] == 0
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_random_block_terrain_matches_oracle(precision):
+    n = 96
+    clip = load_clip(CLIP)
+    terrain = O.Terrain(O.TERRAIN_RANDOM_BLOCKS)
+    env = HumanoidVecEnv(n, clips=(CLIP,), seed=12, precision=precision)
+    env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
+    env.reset()
+    _, book = env.get_state()
+    keys = book[:, BK["terrain_key_lo"]] + book[:, BK["terrain_key_hi"]] * 2.0 ** 32
+    assert len(np.unique(keys)) == n   # every lane its own terrain
+    rng = np.random.default_rng(3)
+    _place(env, terrain, rng, (-25, 25, -25, 25))
+    a = rng.uniform(-1, 1, (n, 17)).astype(np.float32)
+    res = _one_step_vs_oracle(env, terrain, a, clip)
+    assert res["tilted"] > 0, "no contact against a terrain slope was exercised"
+    _check(res, precision)
+    # a rollout with auto-reset (a new terrain per reset), then the one-step comparison again
+    g = torch.Generator(device="cuda").manual_seed(7)
+    for _ in range(40):
+        env.step(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
+    _, book2 = env.get_state()
+    keys2 = book2[:, BK["terrain_key_lo"]] + book2[:, BK["terrain_key_hi"]] * 2.0 ** 32
+    assert (keys2 != keys).any()
+    assert env.error_flags() & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
+    _check(_one_step_vs_oracle(env, terrain, rng.uniform(-1, 1, (n, 17)).astype(np.float32), clip), precision)
+    env.close()
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_ramp_heightfield_matches_oracle(precision):
+    n = 64
+    clip = load_clip(CLIP)
+    h = ramp_heights()
+    terrain = O.Terrain(O.TERRAIN_HEIGHTFIELD, heights=h, w=256, l=256, origin=(0.0, 0.0, 0.25))
+    env = HumanoidVecEnv(n, clips=(CLIP,), seed=5, precision=precision)
+    env.set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=h, w=256, l=256, origin=(0.0, 0.0, 0.25))
+    env.reset()
+    rng = np.random.default_rng(11)
+    _place(env, terrain, rng, (-2.0, 9.0, -4.0, 4.0))
+    a = rng.uniform(-1, 1, (n, 17)).astype(np.float32)
+    res = _one_step_vs_oracle(env, terrain, a, clip)
+    assert res["tilted"] > 0
+    _check(res, precision)
+    env.close()
+
+
+def test_flat_heightfield_steps_like_the_plane():
+    n = 32
+    envs = [HumanoidVecEnv(n, clips=(CLIP,), seed=8, precision="fp64") for _ in range(2)]
+    envs[1].set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=np.zeros(128 * 128), w=128, l=128, origin=(0.0, 0.0, 0.0))
+    g = torch.Generator(device="cuda").manual_seed(2)
+    acts = [(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1) for _ in range(20)]
+    for e in envs:
+        e.reset()
+        for a in acts:
+            e.step(a)
+    p0, b0 = envs[0].get_state()
+    p1, b1 = envs[1].get_state()
+    assert np.abs(p0 - p1).max() < 1e-6
+    for e in envs:
+        e.close()
+
+
+def test_custom_env_view():
+    """LowLevelHumanoidEnv(useCustomEnv=True): random terrain per reset; flat_env.stadium_scene.
+    replaceHeightfieldData installs a heightfield until the next reset (env_vis_low.py:155-171)."""
+    env = LowLevelHumanoidEnv(reference_name=CLIP, useCustomEnv=True, seed=4)
+    obs = env.resetFromFrame(startFrame=0, startFromRef=True, initVel=True)
+    assert obs.shape == (70,)
+    assert env._v.terrain == N.HUM_TERRAIN_RANDOM_BLOCKS
+    env.flat_env.stadium_scene.replaceHeightfieldData(ramp_heights())
+    assert env._v.terrain == N.HUM_TERRAIN_HEIGHTFIELD
+    for _ in range(5):
+        o, r, d, _ = env.step(np.zeros(17, np.float32))
+        assert np.isfinite(o).all()
+    env.reset()
+    assert env._v.terrain == N.HUM_TERRAIN_RANDOM_BLOCKS
+    env.close()
+    with pytest.raises(N.NativeError):
+        HumanoidVecEnv(4, clips=(CLIP,), kernel=0).set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)

@@ -4,7 +4,7 @@
 Compiles humanoid_env.hip for gfx950 with -DHUM_PHASE_MARK -DHUM_DIAG_F32_ONLY (asm comment markers at the
 phase ends of group_substep / the kernel) and counts VALU / LDS / SALU / VMEM instructions between markers;
 loops inside a phase are listed (backward branches) so dynamic counts can be estimated.
-usage: tools/isa_phases.py [out.s]
+usage: [ISA_FLAGS="extra hipcc flags"] tools/isa_phases.py [out.s]
 """
 import collections
 import os
@@ -21,7 +21,8 @@ NAMES = {1: "fk", 2: "pass1", 3: "pass2", 4: "base+pass3", 5: "geom/limits", 6: 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "/tmp/isa_phases.s"
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
-                           "-S", "-DHUM_PHASE_MARK", "-DHUM_DIAG_F32_ONLY", "-o", out, SRC])
+                           "-S", "-DHUM_PHASE_MARK", "-DHUM_DIAG_F32_ONLY", "-o", out, SRC]
+                          + os.environ.get("ISA_FLAGS", "").split())
     lines = open(out).read().split("\n")
     st = [i for i, l in enumerate(lines) if re.match(r"_ZN3hkk17step_group_kernelIfLi4EEEvNS_5KArgsE:", l)][0]
     en = [i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end")][0]
