@@ -115,6 +115,7 @@ struct PostPhys {   // physics-derived quantities calc_state reads (pybullet get
     double bx, by, bz;          // body_xyz
     double roll, pitch, yaw;
     double lin[3];
+    double rfoot[2];            // world x, y of the right foot part (resetFromFrame's starting_ep_pos)
 };
 
 // WalkerBase.calc_state (pybullet_envs/robot_locomotors.py) -> 42 float32 + side effects
@@ -131,6 +132,8 @@ __device__ inline void calc_state(const T* st, const double* wt, float* obs42, f
     pp.bx = pairwise_sum<NPART>([&](int k) -> double { return part_body[k] < 0 ? 0.0 : bpx + (double)parts[k][0]; }) / NPART;
     pp.by = pairwise_sum<NPART>([&](int k) -> double { return part_body[k] < 0 ? 0.0 : bpy + (double)parts[k][1]; }) / NPART;
     pp.bz = (double)st[2];
+    pp.rfoot[0] = bpx + (double)parts[PART_RIGHT_FOOT][0];
+    pp.rfoot[1] = bpy + (double)parts[PART_RIGHT_FOOT][1];
     double qd4[4] = {(double)st[3], (double)st[4], (double)st[5], (double)st[6]};
     euler_from_quat(qd4, pp.roll, pp.pitch, pp.yaw);
     joints_at_limit = 0;

@@ -195,24 +195,15 @@ __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i,
     const double th = (degToTarget + reset_yaw) * DEG2RAD;                  // :272-273 scipy from_euler
     st[3] = 0; st[4] = 0; st[5] = (T)sin(th / 2); st[6] = (T)cos(th / 2);
     b.hldt = degToTarget * DEG2RAD;                                         // :275
-    // starting_ep_pos (:277-289) and the initial base velocity (:291-295)
+    // starting_ep_pos (:277-289) and the initial base velocity (:291-295); the right foot's position comes from
+    // the reset pose's calc_state (:304-305, computed once: the pose is final once the velocity is set)
     const int f0 = b.frame, f1 = (b.frame + 2) % c.max_frame;
     const double phi = degToTarget * DEG2RAD;
     const double qz = sin(phi / 2), qw = cos(phi / 2);
     const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
+    const double* e0 = c.ep + f0 * 27;
+    const double* e1 = c.ep + f1 * 27;
     {
-        Kin<T> K;
-        if (scs && ref) forward_kinematics_pre(st + 3, scs, K);
-        else forward_kinematics(st + 3, st + 13, K);
-        T pp[NPART][3];
-        part_positions(K, pp);
-        const double rfx = (double)st[0] + (double)pp[PART_RIGHT_FOOT][0];
-        const double rfy = (double)st[1] + (double)pp[PART_RIGHT_FOOT][1];
-        const double* e0 = c.ep + f0 * 27;
-        const double* e1 = c.ep + f1 * 27;
-        const double refx = r00 * e0[EP_RIGHT_FOOT] + r01 * e0[EP_RIGHT_FOOT + 1];
-        const double refy = r10 * e0[EP_RIGHT_FOOT] + r11 * e0[EP_RIGHT_FOOT + 1];
-        b.sep[0] = rfx - refx; b.sep[1] = rfy - refy; b.sep[2] = 0;
         const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
         const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
         if (init_vel) {
@@ -221,12 +212,17 @@ __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i,
             st[9] = (T)(((e1[EP_RIGHT_LEG + 2] - e0[EP_RIGHT_LEG + 2]) / 0.0165) / 1.2);
         }
     }
-    b.lts = 0; b.dj = 0; b.dvj = 0; b.bps = 0; b.es = 0; b.jls = 0; b.alive = 0; b.dlts = 0;   // initReward
-    inc_frame(b, c, 2);                                                     // :302
     float js[NDOF];
     int jal;
     PostPhys<T> pp;
     calc_state(st, b.wt, obs, js, jal, pp, ref ? scs : nullptr);            // :304-305
+    {
+        const double refx = r00 * e0[EP_RIGHT_FOOT] + r01 * e0[EP_RIGHT_FOOT + 1];
+        const double refy = r10 * e0[EP_RIGHT_FOOT] + r11 * e0[EP_RIGHT_FOOT + 1];
+        b.sep[0] = pp.rfoot[0] - refx; b.sep[1] = pp.rfoot[1] - refy; b.sep[2] = 0;
+    }
+    b.lts = 0; b.dj = 0; b.dvj = 0; b.bps = 0; b.es = 0; b.jls = 0; b.alive = 0; b.dlts = 0;   // initReward
+    inc_frame(b, c, 2);                                                     // :302
     ref_obs(c, b.frame, obs + 42, ef);
 }
 

@@ -1446,10 +1446,15 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #endif
         {
             // one wave-uniform trip count (the longest env's, in whole rounds of 4 stages): an env past its
-            // own count keeps cycling its rows with updates masked to dl = 0, so the loop has no divergent exits
-            int tmax = total;
+            // own count keeps cycling its rows with updates masked to dl = 0, so the loop has no divergent exits.
+            // Rounds below the shortest env's count need no mask (tmin): they run a copy of the stage without it.
+            int tmax = total, tmin = total;
 #pragma unroll
-            for (int e = 0; e < EPB_; e++) tmax = max(tmax, __builtin_amdgcn_readlane(total, e * GL));
+            for (int e = 0; e < EPB_; e++) {
+                tmax = max(tmax, __builtin_amdgcn_readlane(total, e * GL));
+                tmin = min(tmin, __builtin_amdgcn_readlane(total, e * GL));
+            }
+            tmin &= ~3;
             RowRegs A, B, C, D;
             int oA = pool_off<T>(pbase), oB = pool_off<T>(pbase + 1), oC = pool_off<T>(pbase + 2), oD;
             load(oA, A);
@@ -1459,8 +1464,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             T lnA = T(0), lnB = T(0), lnC = T(0), lnD;
             T sA = row_sum(A.j0 * n0 + A.j1 * n1), sB, sC, sD, dlp = T(0);
             // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read
-            auto stage = [&](int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX, T& sY, T lnX,
-                             T& lnW) {
+            auto stage = [&](auto masked, int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX,
+                             T& sY, T lnX, T& lnW) {
                 oW = X.next3;
                 load(oW, W);
                 lnW = load_ln(X.next3_ln);
@@ -1468,19 +1473,23 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 const T jv = sX + dlp * X.c;
                 const T lo = -(X.mu * lnX), hi = X.hi + X.mu * lnX;
                 const T lsol = med3(X.lam + X.meff * (X.b - jv), lo, hi);   // == clamp: lo <= hi always
-                const T lnew = kk < total ? lsol : X.lam;
+                T lnew = lsol;
+                if constexpr (decltype(masked)::value) lnew = kk < total ? lsol : X.lam;
                 *reinterpret_cast<T*>(const_cast<char*>(lds0) + oX + RO_LAM * sizeof(T)) = lnew;
                 const T dl = lnew - X.lam;
                 n0 += X.m0 * dl;
                 n1 += X.m1 * dl;
                 dlp = dl;
             };
-            for (int k = 0; k < tmax; k += 4) {
-                stage(k, A, B, D, oA, oD, sA, sB, lnA, lnD);
-                stage(k + 1, B, C, A, oB, oA, sB, sC, lnB, lnA);
-                stage(k + 2, C, D, B, oC, oB, sC, sD, lnC, lnB);
-                stage(k + 3, D, A, C, oD, oC, sD, sA, lnD, lnC);
-            }
+            auto round = [&](auto masked, int k) {
+                stage(masked, k, A, B, D, oA, oD, sA, sB, lnA, lnD);
+                stage(masked, k + 1, B, C, A, oB, oA, sB, sC, lnB, lnA);
+                stage(masked, k + 2, C, D, B, oC, oB, sC, sD, lnC, lnB);
+                stage(masked, k + 3, D, A, C, oD, oC, sD, sA, lnD, lnC);
+            };
+            int k = 0;
+            for (; k < tmin; k += 4) round(std::false_type{}, k);
+            for (; k < tmax; k += 4) round(std::true_type{}, k);
         }
     } else {
         // the block's rows overflow its LDS pool: plain loop over pool positions (LDS or global spill region)
