@@ -648,7 +648,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     const unsigned long long t_wave0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt_wave0 = __builtin_amdgcn_s_memrealtime();
 #ifdef HUM_WAVE_LOG
-    if (threadIdx.x < 12) s_phase[threadIdx.x] = 0;
+    if (threadIdx.x < 24) s_phase[threadIdx.x] = 0;
 #endif
 #endif
     load_tab_lds<T>();
@@ -697,6 +697,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         a.agents[i] = 0;
     } else if (valid && l == 0) {
         load_book(a, i, b);
+        SUBPHASE(17);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
             nonfinite_outputs(a, i, b.frame);
@@ -718,6 +719,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             }
         }
     }
+    SUBPHASE(18);
     if (!a.hier) {
         // auto-reset (low-level env): lane 0 draws the start frame (reset_lane's first draw), the env's lanes
         // compute the reset pose's hinge sin / cos, lane 0 finishes reset_lane with them and stores the lane
@@ -775,7 +777,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             g_wave_log[blockIdx.x][6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
             g_wave_log[blockIdx.x][7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
 #ifdef HUM_WAVE_LOG
-            for (int k = 1; k <= 10; k++) g_wave_log[blockIdx.x][8 + k] = (unsigned)s_phase[k];
+            for (int k = 1; k <= 23; k++) g_wave_log[blockIdx.x][8 + k] = (unsigned)s_phase[k];
 #endif
         }
     }

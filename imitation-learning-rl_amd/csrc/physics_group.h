@@ -307,9 +307,10 @@ __host__ __device__ constexpr long gcon_offset(int epb, int cap, int ge) {
 #if defined(HUM_PHASE_TIMING) || defined(HUM_WAVE_LOG)
 #define HUM_WLOG_ON 1
 // per-block work log: [0] s_memtime duration, [1] PGS length, [2] row rounds, [3] narrow-phase rounds,
-// [4] s_memrealtime duration, [5] s_memrealtime start, [6] HW_ID, [7] XCC_ID, [8 + k] phase k cycles
+// [4] s_memrealtime duration, [5] s_memrealtime start, [6] HW_ID, [7] XCC_ID, [8 + k] phase k cycles (k 1-10;
+// 11-23: optional sub-phase markers SUBPHASE(k), which split the time of the phase they sit in)
 // (HUM_WAVE_LOG builds: accumulated in LDS by thread 0, written at the end)
-constexpr int WLOG_W = 20;
+constexpr int WLOG_W = 32;   // [8 + k]: phase k (1-10), sub-phase markers 11-23
 __device__ unsigned g_wave_log[65536][WLOG_W];
 template <int EPB_>
 __device__ inline int env_max(int x) {   // max over the wave's envs of a per-env (group-uniform) value
@@ -338,7 +339,7 @@ __device__ unsigned long long g_phase_cycles[32];
     } while (0)
 #define PHASE_INIT unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
 #elif defined(HUM_WAVE_LOG)
-static __shared__ unsigned long long s_phase[12];
+static __shared__ unsigned long long s_phase[24];
 #define PHASE(k)                                                                 \
     do {                                                                         \
         if (threadIdx.x == 0) {                                                  \
@@ -354,6 +355,12 @@ static __shared__ unsigned long long s_phase[12];
 #else
 #define PHASE(k) do { } while (0)
 #define PHASE_INIT do { } while (0)
+#endif
+
+#if defined(HUM_WAVE_LOG) && defined(HUM_SUBPHASE)   // finer split of a phase's time (tools/wave_log.py)
+#define SUBPHASE(k) PHASE(k)
+#else
+#define SUBPHASE(k) do { } while (0)
 #endif
 
 #ifdef HUM_CHECK_LINKS
@@ -994,11 +1001,13 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             scs[2 * d + 1] = cs;
         }
         wave_sync();
+        SUBPHASE(11);
         T quat[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) quat[e] = S.st[3 + e];
         Kin<T> K;
         forward_kinematics_pre(quat, scs, K);
+        SUBPHASE(12);
         if (l == 0) {
 #pragma unroll
             for (int b = 0; b < NB; b++) {
@@ -1044,6 +1053,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                     for (int e = 0; e < 6; e++) V[e] += Sc[e] * S.nu[6 + d];
             }
         }
+        SUBPHASE(13);
         T cb[6] = {0, 0, 0, 0, 0, 0};
         const int k = body_ndof_l(b), d0 = body_dof0_l(b);
         for (int j = 0; j < k; j++) {
@@ -1084,6 +1094,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         pA[0] -= c3[1] * mg;
         pA[1] -= -c3[0] * mg;
         pA[5] -= mg;
+        SUBPHASE(14);
         for (int q = 0; q < body_nlink_l(b); q++) {   // Bullet per-link velocity damping
             const int lk = body_link0_l(b) + q;
             T cl[3], vc[3], Iw[9], wI[3];
@@ -1158,6 +1169,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (int e = 0; e < 6; e++) A.V[0][e] = a0[e];
         }
         wave_sync();
+        SUBPHASE(15);
         group_fwd_level<T, 0>(P, S, l >> 2, dt);
         wave_sync();
         group_fwd_level<T, 1>(P, S, l >> 2, dt);
@@ -1477,7 +1489,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 if constexpr (decltype(masked)::value) lnew = kk < total ? lsol : X.lam;
                 *reinterpret_cast<T*>(const_cast<char*>(lds0) + oX + RO_LAM * sizeof(T)) = lnew;
                 const T dl = lnew - X.lam;
-                n0 += X.m0 * dl;
+                // the same fma twice, spelled differently: SLP would pack the two into a v_pk_fma_f32 on an
+                // (m0, m1) register pair, which the (J, M^-1 J^T) pair loads never deliver adjacent: the copies
+                // that build the pair waited on the row loads just issued (two exposed LDS latencies per round)
+                n0 = fma(X.m0, dl, n0);
                 n1 += X.m1 * dl;
                 dlp = dl;
             };

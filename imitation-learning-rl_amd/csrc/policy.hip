@@ -6,9 +6,13 @@
 // DiagGaussian(mean, exp(log_std)); RLlib's clip_actions clips the sample to the Box [-1, 1] before env.step.
 // Weights are fp32 [in][out] (the TF kernel layout RLlib's get_weights() returns).
 //
-// MI355X mapping: one 256-thread block = 16 envs x 4 waves.  Layer outputs are 16x16 tiles of
-// v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain), each wave owning a 64-column slice of the layer;
-// activations go through LDS (16 x 256 fp32 = 16 KB), weights stream from L2 (349 KB in all, resident).
+// MI355X mapping: one block = 16 envs x 16 waves (1024 threads; 4096 envs = 256 blocks = one per CU, four waves
+// per SIMD).  Wave w owns the 16x16 output tile of columns 16w..16w+15 of each hidden layer (waves 0, 1 the two
+// tiles of the 17-wide output layer), computed on v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain).
+// Weights are re-laid out once at hum_policy_create into MFMA B-fragment order (per tile, per 4 k-steps, per lane
+// a float4), so a wave fetches a whole layer's operands with coalesced 16-byte loads issued before the first
+// MFMA that needs them; activations go through LDS at a row pitch that keeps the A-fragment reads
+// conflict-free (pitch = 2 mod 32 banks).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -22,9 +26,14 @@ void hum_internal_set_error(const char* msg);
 namespace {
 
 constexpr int OBS = HUM_NOBS, ACT = HUM_NACT, H = 256, K1 = 72;   // K1: 70 padded to a multiple of 4
-constexpr int ROWS = 16, WAVES = 4;
+constexpr int ROWS = 16, WAVES = H / 16;
+// B-fragment layout: [tile][k-step quad][lane][4]; k-steps per layer 18 (K1 / 4, quads padded to 5), 64, 64
+constexpr int SQ1 = 5, SQ2 = 16, SQ3 = 16, NT3 = 2;
+constexpr size_t FRAG1 = (size_t)WAVES * SQ1 * 64 * 4, FRAG2 = (size_t)WAVES * SQ2 * 64 * 4, FRAG3 = (size_t)NT3 * SQ3 * 64 * 4;
+constexpr int PX = 98, PH = 258;   // LDS row pitches (floats): 2 mod 32, so the 32 lanes of a b32 read hit 32 banks
 
 struct PolicyArgs {
+    const float* f1; const float* f2; const float* f3;   // B fragments (frag_layout)
     const float* w1; const float* b1; const float* w2; const float* b2; const float* w3; const float* b3;
     const float* log_std;
     const float* obs; const float* obs_reset; const unsigned char* done;
@@ -42,32 +51,49 @@ __device__ inline unsigned long long mix64(unsigned long long z) {
     return z ^ (z >> 31);
 }
 
-// one 16 x (16 * NT) output slice of X[16 x K] (LDS, row stride ldx) times W[K x ncol] (global, row stride ldw):
-// acc[t] = 16x16 tile t; lane l: A = X[l & 15][4s + (l >> 4)], B = W[4s + (l >> 4)][col0 + 16t + (l & 15)]
-template <int NT>
-__device__ inline void mfma_slice(const float* X, int ldx, int K, const float* __restrict__ W, int ldw, int col0,
-                                  int ncol, f32x4* acc) {
-    const int l = threadIdx.x & 63, r = l & 15, kq = l >> 4;
+// B fragment of k-step s for lane l of a 16-column tile at column c0 of W[K x ncol] (row stride ldw):
+// W[4s + (l >> 4)][c0 + (l & 15)], 0 outside the matrix
+__host__ inline float frag_value(const float* W, int K, int ldw, int ncol, int c0, int s, int l) {
+    const int k = 4 * s + (l >> 4), c = c0 + (l & 15);
+    return k < K && c < ncol ? W[(size_t)k * ldw + c] : 0.f;
+}
+__host__ inline void frag_layout(const float* W, int K, int ldw, int ncol, int ntile, int nsq, float* out) {
+    for (int t = 0; t < ntile; t++)
+        for (int q = 0; q < nsq; q++)
+            for (int l = 0; l < 64; l++)
+                for (int j = 0; j < 4; j++)
+                    out[(((size_t)t * nsq + q) * 64 + l) * 4 + j] = frag_value(W, K, ldw, ncol, 16 * t, 4 * q + j, l);
+}
+
+// the wave's B fragments of one layer (tile t), every load issued at once
+template <int NSQ>
+__device__ inline void load_frags(const float* __restrict__ F, int t, f32x4* b) {
+    const int l = threadIdx.x & 63;
+    const f32x4* src = reinterpret_cast<const f32x4*>(F) + (size_t)t * NSQ * 64 + l;
 #pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < K / 4; s++) {
-        const int k = 4 * s + kq;
-        const float a = X[r * ldx + k];
+    for (int q = 0; q < NSQ; q++) b[q] = src[q * 64];
+}
+// one 16x16 tile: acc = X[16 x 4*NS] (LDS, pitch ldx) times the tile's fragments, k-steps in order
+template <int NS>
+__device__ inline f32x4 mfma_tile(const float* X, int ldx, const f32x4* b) {
+    const int l = threadIdx.x & 63;
+    const float* xr = X + (l & 15) * ldx + (l >> 4);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < NT; t++) {
-            const int c = col0 + 16 * t + r;
-            const float b = c < ncol ? W[(long)k * ldw + c] : 0.f;
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
-        }
-    }
+    for (int s = 0; s < NS; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], b[s >> 2][s & 3], acc, 0, 0, 0);
+    return acc;
 }
 
 __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
-    __shared__ float xs[ROWS][K1];
-    __shared__ float h1[ROWS][H];
-    __shared__ float h2[ROWS][H];
+    __shared__ float xs[ROWS * PX];
+    __shared__ float h1[ROWS * PH];
+    __shared__ float h2[ROWS * PH];
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
     const int row0 = blockIdx.x * ROWS;
+    // every fragment this wave needs, before anything waits (hidden layers: tile = wave; output layer: waves 0, 1)
+    f32x4 b1f[SQ1], b2f[SQ2];
+    load_frags<SQ1>(p.f1, wave, b1f);
+    load_frags<SQ2>(p.f2, wave, b2f);
     // observation tile (done lanes read their post-reset observation: the sampler's next input)
     for (int e = tid; e < ROWS * K1; e += blockDim.x) {
         const int r = e / K1, k = e - r * K1, i = row0 + r;
@@ -76,48 +102,43 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
             const bool rs = p.obs_reset && p.done && p.done[i];
             v = (rs ? p.obs_reset : p.obs)[(long)i * OBS + k];
         }
-        xs[r][k] = v;
+        xs[r * PX + k] = v;
         if (p.obs_in_out && i < p.n && k < OBS) p.obs_in_out[(long)i * OBS + k] = v;
     }
     __syncthreads();
-    f32x4 acc[4];
-    const int col0 = 64 * wave;
-    // C/D map: lane l, register q -> row 4 (l >> 4) + q, column l & 15
-    mfma_slice<4>(&xs[0][0], K1, K1, p.w1, H, col0, H, acc);
+    const int c = 16 * wave + (l & 15);   // C/D map: lane l, register q -> row 4 (l >> 4) + q, column l & 15
+    {
+        const f32x4 acc = mfma_tile<K1 / 4>(xs, PX, b1f);
+        const float bias = p.b1[c];
 #pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = 4 * (l >> 4) + q, c = col0 + 16 * t + (l & 15);
-            h1[r][c] = tanhf(acc[t][q] + p.b1[c]);
-        }
+        for (int q = 0; q < 4; q++) h1[(4 * (l >> 4) + q) * PH + c] = tanhf(acc[q] + bias);
+    }
     __syncthreads();
-    mfma_slice<4>(&h1[0][0], H, H, p.w2, H, col0, H, acc);
+    {
+        const f32x4 acc = mfma_tile<H / 4>(h1, PH, b2f);
+        const float bias = p.b2[c];
 #pragma unroll
-    for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = 4 * (l >> 4) + q, c = col0 + 16 * t + (l & 15);
-            h2[r][c] = tanhf(acc[t][q] + p.b2[c]);
-        }
+        for (int q = 0; q < 4; q++) h2[(4 * (l >> 4) + q) * PH + c] = tanhf(acc[q] + bias);
+    }
     __syncthreads();
-    if (wave < 2) {   // output layer: 17 columns = two 16-wide tiles, one per wave
-        f32x4 o[1];
-        mfma_slice<1>(&h2[0][0], H, H, p.w3, ACT, 16 * wave, ACT, o);
+    if (wave < NT3) {   // output layer: 17 columns = two 16-wide tiles, one per wave
+        f32x4 b3f[SQ3];
+        load_frags<SQ3>(p.f3, wave, b3f);
+        const f32x4 o = mfma_tile<H / 4>(h2, PH, b3f);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const int r = 4 * (l >> 4) + q, c = 16 * wave + (l & 15), i = row0 + r;
-            if (c < ACT && i < p.n) {
-                const float mean = o[0][q] + p.b3[c];
+            const int r = 4 * (l >> 4) + q, c3 = 16 * wave + (l & 15), i = row0 + r;
+            if (c3 < ACT && i < p.n) {
+                const float mean = o[q] + p.b3[c3];
                 float a = mean;
                 if (p.explore) {   // DiagGaussian sample: mean + exp(log_std) * N(0, 1), counter-based Box-Muller
-                    const unsigned long long x = mix64(p.seed ^ mix64(((unsigned long long)i << 32) ^ (p.step * 32 + c)));
+                    const unsigned long long x = mix64(p.seed ^ mix64(((unsigned long long)i << 32) ^ (p.step * 32 + c3)));
                     const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;   // (0, 1]
                     const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
-                    a = mean + expf(p.log_std[c]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+                    a = mean + expf(p.log_std[c3]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
                 }
-                p.act[(long)i * ACT + c] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
-                if (p.mean_out) p.mean_out[(long)i * ACT + c] = mean;
+                p.act[(long)i * ACT + c3] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
+                if (p.mean_out) p.mean_out[(long)i * ACT + c3] = mean;
             }
         }
     }
@@ -127,8 +148,8 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
 
 struct hum_policy {
     int device;
-    float* w;   // one allocation: w1 b1 w2 b2 w3 b3 log_std
-    const float *w1, *b1, *w2, *b2, *w3, *b3, *log_std;
+    float* w;   // one allocation: w1 b1 w2 b2 w3 b3 log_std, then the B fragments of w1, w2, w3
+    const float *w1, *b1, *w2, *b2, *w3, *b3, *log_std, *f1, *f2, *f3;
     unsigned long long seed;
 };
 
@@ -147,7 +168,8 @@ int hum_policy_create(int32_t device, const float* w1, const float* b1, const fl
     if (hipSetDevice(device) != hipSuccess) return perr(HUM_ERR_HIP, "hum_policy_create: hipSetDevice");
     // w1 is stored padded to K1 rows (rows 70, 71 zero) so the kernel's k loop needs no bound
     const size_t n1 = (size_t)K1 * H, n2 = (size_t)H * H, n3 = (size_t)H * ACT;
-    const size_t total = n1 + H + n2 + H + n3 + ACT + ACT;
+    const size_t nw = (n1 + H + n2 + H + n3 + ACT + ACT + 63) / 64 * 64;   // fragments 16-byte aligned
+    const size_t total = nw + FRAG1 + FRAG2 + FRAG3;
     hum_policy* p = new hum_policy();
     p->device = device;
     p->seed = seed;
@@ -164,6 +186,9 @@ int hum_policy_create(int32_t device, const float* w1, const float* b1, const fl
     std::memcpy(h + o, w3, n3 * sizeof(float)); o += n3;
     std::memcpy(h + o, b3, ACT * sizeof(float)); o += ACT;
     if (log_std) std::memcpy(h + o, log_std, ACT * sizeof(float));
+    frag_layout(w1, OBS, H, H, WAVES, SQ1, h + nw);
+    frag_layout(w2, H, H, H, WAVES, SQ2, h + nw + FRAG1);
+    frag_layout(w3, H, ACT, ACT, NT3, SQ3, h + nw + FRAG1 + FRAG2);
     const hipError_t st = hipMemcpy(p->w, h, total * sizeof(float), hipMemcpyHostToDevice);
     delete[] h;
     if (st != hipSuccess) {
@@ -173,6 +198,7 @@ int hum_policy_create(int32_t device, const float* w1, const float* b1, const fl
     }
     p->w1 = p->w; p->b1 = p->w1 + n1; p->w2 = p->b1 + H; p->b2 = p->w2 + n2; p->w3 = p->b2 + H;
     p->b3 = p->w3 + n3; p->log_std = p->b3 + ACT;
+    p->f1 = p->w + nw; p->f2 = p->f1 + FRAG1; p->f3 = p->f2 + FRAG2;
     *out = p;
     return HUM_OK;
 }
@@ -191,6 +217,7 @@ int hum_policy_act(hum_policy* p, const float* obs, const float* obs_reset, cons
     if ((obs_reset == nullptr) != (done == nullptr)) return perr(HUM_ERR_ARG, "hum_policy_act: obs_reset needs done");
     if (hipSetDevice(p->device) != hipSuccess) return perr(HUM_ERR_HIP, "hum_policy_act: hipSetDevice");
     PolicyArgs a;
+    a.f1 = p->f1; a.f2 = p->f2; a.f3 = p->f3;
     a.w1 = p->w1; a.b1 = p->b1; a.w2 = p->w2; a.b2 = p->b2; a.w3 = p->w3; a.b3 = p->b3; a.log_std = p->log_std;
     a.obs = obs; a.obs_reset = obs_reset; a.done = done; a.act = actions; a.mean_out = mean_out; a.obs_in_out = obs_in_out;
     a.n = n; a.explore = explore; a.seed = p->seed; a.step = step;

@@ -18,13 +18,13 @@ pool = [(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1) for _ in range(8
 for s in range(10):
     env.step(pool[s % 8], autoreset=True)
 rows = []
-buf = np.zeros((nb, 20), np.uint32)
+buf = np.zeros((nb, 32), np.uint32)
 for s in range(30):
     L.hum_debug_wave_log(None, nb, 1)
     _, _, done, _ = env.step(pool[s % 8], autoreset=True)
     L.hum_debug_wave_log(buf.ctypes.data, nb, 0)
     d = done.cpu().numpy().reshape(nb, 4).sum(1)
-    rows.append(np.column_stack([buf[:, :5].astype(np.float64), d, np.full(nb, s), buf[:, 9:19].astype(np.float64)]))
+    rows.append(np.column_stack([buf[:, :5].astype(np.float64), d, np.full(nb, s), buf[:, 9:32].astype(np.float64)]))
     st = buf[:, 5].astype(np.int64)
     st = (st - st.min()) % (1 << 32)
     hw = buf[:, 6].astype(np.int64)
@@ -73,5 +73,12 @@ top = dur >= np.quantile(dur, 0.99)
 print("phase cycles per block-step: mean | slowest 1%% | corr with duration")
 for k in range(10):
     print("  %-12s %8.0f | %8.0f | %.2f" % (pn[k], ph[:, k].mean(), ph[top, k].mean(), np.corrcoef(ph[:, k], dur)[0, 1]))
+sub = X[:, 17:30]   # sub-phase markers 11-23 (HUM_SUBPHASE builds): time from the previous marker
+subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1: inertia+bias", 15: "pass3: base",
+        17: "post: book load", 18: "post: post_step"}
+if sub.any():
+    print("sub-phase cycles per block-step (each taken out of its phase above): mean | slowest 1%")
+    for k, nm in subn.items():
+        print("  %-22s %8.0f | %8.0f" % (nm, sub[:, k - 11].mean(), sub[top, k - 11].mean()))
 pg = ph[:, 7] / np.maximum(X[:, 1], 1)
 print("pgs cycles per unit pgs_len: mean %.0f (per row-iteration at 5 iters: %.0f)" % (pg.mean(), pg.mean() / 5))
