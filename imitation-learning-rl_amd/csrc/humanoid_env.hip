@@ -205,11 +205,14 @@ int hum_create(const hum_config* cfg, hum_env** out) {
     }
     if (st == hipSuccess) st = hipMalloc((void**)&e->eflags, sizeof(unsigned));
     if (st == hipSuccess) st = hipMalloc((void**)&e->clips_dev, HUM_MAX_CLIPS * sizeof(ClipDev));
-    if (st == hipSuccess) st = hipMemset(e->clips_dev, 0, HUM_MAX_CLIPS * sizeof(ClipDev));
-    if (st == hipSuccess) st = hipMemset(e->d.bi, 0, NBOOK_I * n * sizeof(int));
-    if (st == hipSuccess) st = hipMemset(e->d.bd, 0, NBOOK_D * n * sizeof(double));
-    if (st == hipSuccess) st = hipMemset(e->d.phys, 0, HUM_NSTATE * n * e->real_size);
-    if (st == hipSuccess) st = hipMemset(e->eflags, 0, sizeof(unsigned));
+    // zero-fill on the handle's own stream, so it is ordered before init_kernel: a plain hipMemset goes to the
+    // null stream, which a non-blocking stream does not wait for, and a fill landing after init_kernel erased the
+    // lanes' RNG keys (seen as an intermittent mismatch in test_gpu_multiproc)
+    if (st == hipSuccess) st = hipMemsetAsync(e->clips_dev, 0, HUM_MAX_CLIPS * sizeof(ClipDev), e->stream);
+    if (st == hipSuccess) st = hipMemsetAsync(e->d.bi, 0, NBOOK_I * n * sizeof(int), e->stream);
+    if (st == hipSuccess) st = hipMemsetAsync(e->d.bd, 0, NBOOK_D * n * sizeof(double), e->stream);
+    if (st == hipSuccess) st = hipMemsetAsync(e->d.phys, 0, HUM_NSTATE * n * e->real_size, e->stream);
+    if (st == hipSuccess) st = hipMemsetAsync(e->eflags, 0, sizeof(unsigned), e->stream);
     if (st == hipSuccess) {
         KArgs a = make_args(e);
         hipLaunchKernelGGL(init_kernel, grid_of(e), dim3(e->cfg.block_size), 0, e->stream, a);
@@ -670,7 +673,8 @@ int hum_get_error_flags(hum_env* e, uint32_t* flags) {
     HIPCHK(hipDeviceSynchronize());
     unsigned v = 0;
     HIPCHK(hipMemcpy(&v, e->eflags, sizeof v, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemset(e->eflags, 0, sizeof v));
+    HIPCHK(hipMemsetAsync(e->eflags, 0, sizeof v, e->stream));   // done before any later launch (see hum_create)
+    HIPCHK(hipStreamSynchronize(e->stream));
     *flags = v;
     return HUM_OK;
 }

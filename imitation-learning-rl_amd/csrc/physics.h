@@ -129,6 +129,27 @@ __device__ inline void quat_to_mat(const T* q, T* R) {
 template <typename T>
 __device__ inline T clampT(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// Physics-only fp32 reciprocal / square root / reciprocal square root on the hardware instructions (v_rcp_f32,
+// v_sqrt_f32, v_rsq_f32: 1 ulp) instead of the ~10-instruction correctly rounded sequences, which sat on the
+// dependent chains of the base Cholesky, the ABA pivots, the row scalings and the narrow phase (+1.5% measured).
+// The physics is held to a tolerance against the fp64 oracle, not to bits; fp64 stays IEEE.  The env logic
+// (rewards, observations) never uses these.
+template <typename T>
+__device__ inline T prcp(T x) {
+    if constexpr (sizeof(T) == 4) return __builtin_amdgcn_rcpf(x);
+    else return T(1) / x;
+}
+template <typename T>
+__device__ inline T psqrt(T x) {
+    if constexpr (sizeof(T) == 4) return __builtin_amdgcn_sqrtf(x);
+    else return sqrt(x);
+}
+template <typename T>
+__device__ inline T prsqrt(T x) {
+    if constexpr (sizeof(T) == 4) return __builtin_amdgcn_rsqf(x);
+    else return T(1) / sqrt(x);
+}
+
 // ------------------------------------------------------------------------------------- kinematics
 template <typename T>
 struct Kin {
@@ -207,16 +228,16 @@ struct Aba {
 template <typename T, int K3>
 __device__ inline void small_inverse(const T* D, T* Di) {  // symmetric k x k (k = K3), stored 3x3
     if constexpr (K3 == 1) {
-        Di[0] = T(1) / D[0];
+        Di[0] = prcp(D[0]);
     } else if constexpr (K3 == 2) {
         T det = D[0] * D[4] - D[1] * D[3];
-        T id = T(1) / det;
+        T id = prcp(det);
         Di[0] = D[4] * id; Di[1] = -D[1] * id; Di[3] = -D[3] * id; Di[4] = D[0] * id;
     } else {
         T a = D[0], b = D[1], c = D[2], e = D[4], f = D[5], i = D[8];
         T A = e * i - f * f, B = c * f - b * i, C = b * f - c * e;
         T det = a * A + b * B + c * C;
-        T id = T(1) / det;
+        T id = prcp(det);
         Di[0] = A * id; Di[1] = B * id; Di[2] = C * id;
         Di[3] = B * id; Di[4] = (a * i - c * c) * id; Di[5] = (b * c - a * f) * id;
         Di[6] = C * id; Di[7] = (b * c - a * f) * id; Di[8] = (a * e - b * b) * id;
@@ -598,16 +619,17 @@ __device__ inline void seg_seg(const T* p1, const T* q1, const T* p2, const T* q
     T s, t;
     const T EPS = (T)1e-12;
     if (a <= EPS && e <= EPS) { s = t = 0; }
-    else if (a <= EPS) { s = 0; t = clampT(f / e, T(0), T(1)); }
+    else if (a <= EPS) { s = 0; t = clampT(f * prcp(e), T(0), T(1)); }
     else {
         T c = dot3(d1, r);
-        if (e <= EPS) { t = 0; s = clampT(-c / a, T(0), T(1)); }
+        const T ia = prcp(a);
+        if (e <= EPS) { t = 0; s = clampT(-c * ia, T(0), T(1)); }
         else {
             T b = dot3(d1, d2), den = a * e - b * b;
-            s = (den > EPS) ? clampT((b * f - c * e) / den, T(0), T(1)) : T(0);
-            t = (b * s + f) / e;
-            if (t < 0) { t = 0; s = clampT(-c / a, T(0), T(1)); }
-            else if (t > 1) { t = 1; s = clampT((b - c) / a, T(0), T(1)); }
+            s = (den > EPS) ? clampT((b * f - c * e) * prcp(den), T(0), T(1)) : T(0);
+            t = (b * s + f) * prcp(e);
+            if (t < 0) { t = 0; s = clampT(-c * ia, T(0), T(1)); }
+            else if (t > 1) { t = 1; s = clampT((b - c) * ia, T(0), T(1)); }
         }
     }
 #pragma unroll
@@ -617,11 +639,11 @@ __device__ inline void seg_seg(const T* p1, const T* q1, const T* p2, const T* q
 template <typename T>
 __device__ inline void plane_space(const T* n, T* p, T* q) {  // btPlaneSpace1
     if (fabs(n[2]) > (T)0.7071067811865475244) {
-        T a = n[1] * n[1] + n[2] * n[2], k = T(1) / sqrt(a);
+        T a = n[1] * n[1] + n[2] * n[2], k = prsqrt(a);
         p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
         q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
     } else {
-        T a = n[0] * n[0] + n[1] * n[1], k = T(1) / sqrt(a);
+        T a = n[0] * n[0] + n[1] * n[1], k = prsqrt(a);
         p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
         q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
     }

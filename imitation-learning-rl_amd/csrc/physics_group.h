@@ -408,7 +408,7 @@ __device__ inline void chol6_inv(const T* A, T* L) {
         T s = A[sidx(j, j)];
 #pragma unroll
         for (int k = 0; k < j; k++) s -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
-        const T inv = T(1) / sqrt(s);
+        const T inv = prsqrt(s);
         L[j * (j + 1) / 2 + j] = inv;
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
@@ -662,6 +662,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                                                           const T dt, int& pbase, int& ptot) {
     const ModelTab<T>& M = tab<T>();
     const int lane = threadIdx.x & 63, cap = P.lds_rows;
+    const T idt = T(1) / dt;
     // pre: task prefix (actual rows); pos: pool prefix (short envs are padded with zero rows, see PGS)
     int cnt[EPB_], nls[EPB_], ncs[EPB_], pre[EPB_ + 1], pos[EPB_ + 1];
     pre[0] = 0;
@@ -707,7 +708,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
             jd = d;
             jsign = sg;
-            sc[0] = -pen * (T)P.erp_limit / dt;
+            sc[0] = -pen * (T)P.erp_limit * idt;
             sc[2] = (T)P.limit_max_impulse;
             sc[5] = 0;
         } else {
@@ -742,7 +743,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 for (int i = 0; i < 3; i++) lat[i] = vr[i] - n[i] * vn;
                 const T l2 = dot3(lat, lat);
                 if (l2 > (T)1e-12) {
-                    const T il = T(1) / sqrt(l2);
+                    const T il = prsqrt(l2);
 #pragma unroll
                     for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
                     cross3(t1, n, t2);
@@ -757,7 +758,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 cross3(pb, dir, fb);
                 fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
             }
-            sc[0] = f == 0 ? (d > 0 ? -d / dt : -d * (T)P.erp_contact / dt) : T(0);
+            sc[0] = f == 0 ? (d > 0 ? -d * idt : -d * (T)P.erp_contact * idt) : T(0);
             sc[2] = f == 0 ? (T)1e10 : T(0);   // friction rows: bounds come from mu * lambda_n in the PGS
             sc[5] = f == 0 ? T(0) : (bb >= 0 ? (T)P.mu_self : (T)P.mu_ground);   // friction rows only
         }
@@ -771,7 +772,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];   // limit rows: sg * Mi[6 + d] (sg^2 = 1)
         sc[1] = 0;   // lo = 0 for every row type: the PGS reads this slot as its zero pad
         sc[3] = 0;
-        sc[4] = T(1) / jm;
+        sc[4] = prcp(jm);
         const int p = epos + pool_pos(r, enl, enc);
         if (p < cap) {
             int n3, n3ln;
@@ -1103,8 +1104,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             cross3(V, cl, vc);
 #pragma unroll
             for (int i = 0; i < 3; i++) vc[i] += V[3 + i];
-            const T kv = (T)P.lin_damp * (T(1) + sqrt(dot3(vc, vc)));
-            const T kw = (T)P.ang_damp * (T(1) + sqrt(dot3(V, V)));
+            const T kv = (T)P.lin_damp * (T(1) + psqrt(dot3(vc, vc)));
+            const T kw = (T)P.ang_damp * (T(1) + psqrt(dot3(V, V)));
             {
                 T RI[9];
 #pragma unroll
@@ -1342,12 +1343,12 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 seg_seg(C.gp[ga][0], C.gp[ga][1], C.gp[gb][0], C.gp[gb][1], ca, cb);
 #pragma unroll
                 for (int i = 0; i < 3; i++) dv[i] = ca[i] - cb[i];
-                const T dist = sqrt(dot3(dv, dv));
+                const T dist = psqrt(dot3(dv, dv));
                 const T ra = geom_r_l<T>(ga), rb = geom_r_l<T>(gb);
                 d = dist - ra - rb;
                 hit = d < (T)P.contact_thresh && dist > (T)1e-9;
                 if (hit) {
-                    const T idist = T(1) / dist;
+                    const T idist = prcp(dist);
 #pragma unroll
                     for (int i = 0; i < 3; i++) {
                         n[i] = dv[i] * idist;
