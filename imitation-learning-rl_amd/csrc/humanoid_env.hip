@@ -81,6 +81,7 @@ KArgs make_args(hum_env* e) {
     a.P.iters = c.solver_iters;
     a.P.erp_contact = c.erp_contact;
     a.P.erp_limit = c.erp_limit;
+    a.P.split_pen = c.split_penetration;
     a.P.mu_ground = c.mu_ground;
     a.P.mu_self = c.mu_self;
     a.P.contact_thresh = c.contact_thresh;
@@ -168,6 +169,7 @@ void hum_default_config(hum_config* c) {
     c->envs_per_block = 4;
     c->lds_rows = 0;
     c->numpy_semantics = HUM_NUMPY_1;
+    c->split_penetration = -0.04;
 }
 
 int hum_create(const hum_config* cfg, hum_env** out) {

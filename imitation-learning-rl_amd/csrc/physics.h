@@ -27,6 +27,7 @@ struct PhysParams {
     double gravity;
     int iters;
     double erp_contact, erp_limit, mu_ground, mu_self, contact_thresh;
+    double split_pen;     // split-impulse threshold: rows penetrating deeper get no position bias (hum_config)
     double lin_damp, ang_damp, limit_max_impulse, max_coord_vel;
     int max_contacts;
     int self_collision;
@@ -687,7 +688,7 @@ __device__ inline int substep(const PhysParams& P, T* st, const T* tau, const La
                 T jm = sg * M[6 + j];
 #pragma unroll
                 for (int e = 0; e < NV; e++) { R(row, E_J + e) = (e == 6 + j) ? sg : T(0); R(row, E_M + e) = M[e]; }
-                R(row, E_B) = -pen * (T)P.erp_limit / dt;
+                R(row, E_B) = pen > (T)P.split_pen ? -pen * (T)P.erp_limit / dt : T(0);
                 R(row, E_LO) = 0;
                 R(row, E_HI) = (T)P.limit_max_impulse;
                 R(row, E_LAM) = 0;
@@ -834,7 +835,7 @@ __device__ inline int substep(const PhysParams& P, T* st, const T* tau, const La
             const int row = f == 0 ? MAX_LIMIT_ROWS + c : MAX_LIMIT_ROWS + MAXC + 2 * c + (f - 1);
 #pragma unroll
             for (int e = 0; e < NV; e++) { R(row, E_J + e) = J[e]; R(row, E_M + e) = M[e]; jm += J[e] * M[e]; }
-            R(row, E_B) = f == 0 ? (d > 0 ? -d / dt : -d * (T)P.erp_contact / dt) : T(0);
+            R(row, E_B) = f == 0 ? (d > 0 ? -d / dt : (d > (T)P.split_pen ? -d * (T)P.erp_contact / dt : T(0))) : T(0);
             R(row, E_LO) = 0;
             R(row, E_HI) = (T)1e10;
             R(row, E_LAM) = 0;

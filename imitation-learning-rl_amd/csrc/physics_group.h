@@ -708,7 +708,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             const T pen = side == 0 ? q - M.lo[d] : M.hi[d] - q;
             jd = d;
             jsign = sg;
-            sc[0] = -pen * (T)P.erp_limit * idt;
+            sc[0] = pen > (T)P.split_pen ? -pen * (T)P.erp_limit * idt : T(0);
             sc[2] = (T)P.limit_max_impulse;
             sc[5] = 0;
         } else {
@@ -758,7 +758,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 cross3(pb, dir, fb);
                 fb[0] = -fb[0]; fb[1] = -fb[1]; fb[2] = -fb[2]; fb[3] = -dir[0]; fb[4] = -dir[1]; fb[5] = -dir[2];
             }
-            sc[0] = f == 0 ? (d > 0 ? -d * idt : -d * (T)P.erp_contact * idt) : T(0);
+            sc[0] = f == 0 ? (d > 0 ? -d * idt : (d > (T)P.split_pen ? -d * (T)P.erp_contact * idt : T(0))) : T(0);
             sc[2] = f == 0 ? (T)1e10 : T(0);   // friction rows: bounds come from mu * lambda_n in the PGS
             sc[5] = f == 0 ? T(0) : (bb >= 0 ? (T)P.mu_self : (T)P.mu_ground);   // friction rows only
         }

@@ -8,7 +8,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
-HUM_ABI_VERSION = 6   # include/humanoid_env.h
+HUM_ABI_VERSION = 7   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
@@ -54,7 +54,7 @@ class HumConfig(ctypes.Structure):
                 ("max_contacts", ctypes.c_int32), ("self_collision", ctypes.c_int32),
                 ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32),
                 ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32), ("lds_rows", ctypes.c_int32),
-                ("numpy_semantics", ctypes.c_int32)]
+                ("numpy_semantics", ctypes.c_int32), ("split_penetration", ctypes.c_double)]
 
 
 class NativeError(RuntimeError):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 6
+#define HUM_ABI_VERSION 7
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -156,6 +156,11 @@ typedef struct hum_config {
                                  pool (envs_per_block * 30), k > 0 caps it at k rows so the rest take the global
                                  spill path (testing) */
     int32_t numpy_semantics;  /* HUM_NUMPY_1 (default) or HUM_NUMPY_2, see above */
+    double split_penetration; /* -0.04: Bullet's split impulse (btContactSolverInfo m_splitImpulse on,
+                                 m_splitImpulsePenetrationThreshold -0.04).  A joint-limit or contact row whose
+                                 penetration is deeper than this carries no position bias, only the velocity
+                                 term: its position part goes to m_rhsPenetration, which btMultiBodyConstraintSolver
+                                 never applies to multibodies.  -1e30 = every violation corrected at ERP */
 } hum_config;
 
 /* Version / build info. */

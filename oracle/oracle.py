@@ -68,7 +68,7 @@ class OmParams(ctypes.Structure):
                 # ground: 0 plane, 1 heightfield hf, 2 CustomScene random blocks (physics_oracle.c terrain_contact)
                 ("terrain", ctypes.c_int), ("hf", ctypes.c_void_p), ("hf_w", ctypes.c_int), ("hf_l", ctypes.c_int),
                 ("hf_s", ctypes.c_double * 3), ("hf_o", ctypes.c_double * 3), ("hf_mid", ctypes.c_double),
-                ("terrain_key", ctypes.c_uint64)]
+                ("terrain_key", ctypes.c_uint64), ("split_pen", ctypes.c_double)]
 
 
 TERRAIN_PLANE, TERRAIN_HEIGHTFIELD, TERRAIN_RANDOM_BLOCKS = 0, 1, 2

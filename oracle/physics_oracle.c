@@ -19,7 +19,8 @@
  *        velocities <- velocities + dt * accelerations (btMultiBody semi-implicit Euler)
  *     3. constraint rows built on those velocities, btMultiBodyConstraintSolver order:
  *        joint-limit rows (violated limits only, erp 0.2, impulse <= 100), contact normal rows
- *        (erp 0.9 = setDefaultContactERP, speculative -d/dt when separated), two friction rows per
+ *        (erp 0.9 = setDefaultContactERP, speculative -d/dt when separated; a limit or contact deeper than
+ *        Bullet's split-impulse threshold -0.04 gets no position bias), two friction rows per
  *        contact (mu = 2.0*0.8 ground / 2.0*2.0 self, box bounds +-mu*lambda_n); PGS, 5 iterations;
  *        the constraint responses use the joint-space mass matrix H (built from link Jacobians) and
  *        its Cholesky factor - an independent route to the same M^-1 J^T the product kernel gets
@@ -35,6 +36,7 @@
 #include <string.h>
 
 #include "humanoid_links_gen.h"
+#include "physics_oracle.h"
 
 #define NV (6 + OM_ND)
 /* contact list capacity: every candidate fits (29 sphere / capsule-end ground points + 66 geom pairs = 95), so
@@ -42,25 +44,6 @@
 #define MAXC 95
 #define MAXROW (3 * MAXC + 2 * OM_ND)
 
-typedef struct {
-    double dt;              /* substep */
-    int nsub;               /* substeps per env step */
-    double gravity;
-    int iters;              /* PGS iterations */
-    double erp_contact, erp_limit, mu_ground, mu_self, contact_thresh;
-    double lin_damp, ang_damp, limit_max_impulse;
-    int max_contacts;
-    int self_collision;
-    int joint_damping;      /* 0: ignore MJCF joint damping, 1: implicit per substep (default) */
-    double max_coord_vel;   /* btMultiBody::m_maxCoordinateVelocity clamp in applyDeltaVeeMultiDof */
-    /* ground (hum_set_terrain): 0 = plane z = 0, 1 = heightfield hf, 2 = CustomScene random blocks from
-       terrain_key (humanoid.py:68-144) */
-    int terrain;
-    const float* hf;        /* terrain 1: heights, vertex (i, j) = hf[i + j * hf_w] */
-    int hf_w, hf_l;
-    double hf_s[3], hf_o[3], hf_mid;
-    unsigned long long terrain_key;
-} om_params;
 
 /* ------------------------------------------------------------------------- small linear algebra */
 static void mat3_mul(const double* A, const double* B, double* C) {
@@ -694,7 +677,7 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
             memset(r->J, 0, sizeof r->J);
             r->J[6 + j] = side == 0 ? 1.0 : -1.0;
             r->kind = 0; r->lo = 0; r->hi = P->limit_max_impulse;
-            r->b = -pen * P->erp_limit / dt;
+            r->b = pen > P->split_pen ? -pen * P->erp_limit / dt : 0.0;
         }
     }
     int first_normal = nr;
@@ -709,7 +692,7 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
         om_row* r = &rows[nr++];
         for (int a = 0; a < NV; a++) r->J[a] = c->n[0] * Jp[a] + c->n[1] * Jp[NV + a] + c->n[2] * Jp[2 * NV + a];
         r->kind = 1; r->lo = 0; r->hi = 1e10;
-        r->b = c->d > 0 ? -c->d / dt : -c->d * P->erp_contact / dt;
+        r->b = c->d > 0 ? -c->d / dt : (c->d > P->split_pen ? -c->d * P->erp_contact / dt : 0.0);
         r->mu = c->mu;
     }
     int first_fric = nr;
@@ -817,6 +800,7 @@ void om_default_params(om_params* P) {
     P->hf_o[2] = 0.25;
     P->hf_mid = 0.25;
     P->terrain_key = 0;
+    P->split_pen = -0.04;
 }
 
 /* one env step of physics: state (47) in place; tau_motor[17] in dof order (already 0.41*power*clip(a)). */

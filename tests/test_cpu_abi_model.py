@@ -51,6 +51,7 @@ def test_default_config_values():
     P = O.default_params()
     assert P.max_contacts == c.max_contacts and P.erp_limit == c.erp_limit and P.contact_thresh == c.contact_thresh
     assert P.limit_max_impulse == c.limit_max_impulse and P.max_coord_vel == c.max_coord_vel
+    assert P.split_pen == c.split_penetration == -0.04
 
 
 def test_product_model_matches_oracle_model():
