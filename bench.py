@@ -82,21 +82,32 @@ def cpu_baseline(seconds, threads):
                       "resets (%d steps)" % (threads, seconds, steps)}
 
 
-def parity_sample(env, clips, per_clip=64, seed=5):
-    """CPU checker leg: from the benchmark's own mid-rollout state, step once more on the GPU (no auto-reset)
-    and compare a sample of lanes per clip with the oracle stepped from the same injected state (one env
-    step: fp64 C physics + the env logic).  Runs after the timed region."""
+def parity_sample(env, clips, per_clip=64, seed=5, sens_bound=1e-5):
+    """CPU checker leg (after the timed region): from the benchmark's own mid-rollout state, step once more on the
+    GPU (no auto-reset) with the benchmarked fp32 kernel AND with the fp64 kernel given the identical state, and
+    compare a sample of lanes per clip with the fp64 oracle stepped from the same injected state (fp64 C physics +
+    the env logic).  Each lane's conditioning is measured too: the oracle stepped again from the state perturbed by
+    2^-24 relative (float32 rounding) - a joint limit or contact that switches on within that margin makes the step
+    discontinuous, and such lanes are reported apart (the error there is the model's, not the kernel's)."""
     import numpy as np
     import torch
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from ilrl_amd import _native as N
     from ilrl_amd.clips import load_clip
+    from ilrl_amd.vec_env import HumanoidVecEnv
     phys, book = env.get_state()
     n = env.n
     a = np.random.default_rng(seed).uniform(-1, 1, (n, 17)).astype(np.float32)
-    obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device=env.device))]
-    eo, er, dm, fm, lanes = [], [], 0, 0, 0
+    at = torch.as_tensor(a, device=env.device)
+    obs, rew, done, frame = [x.cpu().numpy() for x in env.step(at)]
+    env64 = HumanoidVecEnv(n, clips=clips, seed=0, device=env.device.index, precision="fp64")
+    env64.set_state(phys, book)
+    obs64, rew64, done64, _ = [x.cpu().numpy() for x in env64.step(at)]
+    st64, _ = env64.get_state()
+    env64.close()
+    prng = np.random.default_rng(seed + 1)
+    eo, er, e64, r64, s64, sens, dm, fm, dm64, lanes = [], [], [], [], [], [], 0, 0, 0, 0
     for c, name in enumerate(clips):
         idx = np.nonzero(book[:, N.BK["clip"]].astype(int) == c)[0]
         if name == "motion13_13":   # the reference raises IndexError past the 120-row velocity table
@@ -107,14 +118,28 @@ def parity_sample(env, clips, per_clip=64, seed=5):
             ro, rr, rd, _ = o.step(a[i])
             eo.append(float(np.abs(obs[i] - ro).max()))
             er.append(abs(float(rew[i]) - rr))
+            e64.append(float(np.abs(obs64[i] - ro).max()))
+            r64.append(abs(float(rew64[i]) - rr))
+            s64.append(float(np.abs(st64[i] - o.state).max()))
             dm += int(bool(done[i]) != rd)
+            dm64 += int(bool(done64[i]) != rd)
             fm += int(int(frame[i]) != o.frame)
+            p = O.OracleLowLevelEnv.from_lane(clip, phys[i] * (1 + 2.0 ** -24 * prng.choice([-1.0, 1.0], 47)), book[i],
+                                              N.BK)
+            sens.append(float(np.abs(p.step(a[i])[0] - ro).max()))
             lanes += 1
-    eo, er = np.array(eo), np.array(er)
+    eo, er, sens = np.array(eo), np.array(er), np.array(sens)
+    good = sens <= sens_bound
     return {"vs": "fp64 CPU oracle, one env step from the benchmark's own mid-rollout lane states (PyBullet absent: "
-                  "parity vs PyBullet unpinned)", "lanes": lanes, "obs_max_abs_err": float(eo.max()),
-            "obs_p99_abs_err": float(np.percentile(eo, 99)), "reward_max_abs_err": float(er.max()),
-            "done_mismatches": dm, "frame_mismatches": fm}
+                  "parity vs PyBullet unpinned)", "lanes": lanes,
+            "obs_max_abs_err": float(eo.max()), "obs_p99_abs_err": float(np.percentile(eo, 99)),
+            "reward_max_abs_err": float(er.max()), "done_mismatches": dm, "frame_mismatches": fm,
+            "ill_conditioned_lanes": int((~good).sum()),
+            "obs_max_abs_err_conditioned": float(eo[good].max()) if good.any() else None,
+            "reward_max_abs_err_conditioned": float(er[good].max()) if good.any() else None,
+            "conditioning": "oracle obs change under a 2^-24 relative input perturbation > %g" % sens_bound,
+            "fp64_kernel": {"obs_max_abs_err": float(max(e64)), "reward_max_abs_err": float(max(r64)),
+                            "state_max_abs_err": float(max(s64)), "done_mismatches": dm64}}
 
 
 def _load_json(path):

@@ -122,8 +122,15 @@ def test_env_logic_matches_reference_fp32(golden, name, kernel):
     np.testing.assert_array_equal(o["done"], r["done"])
     np.testing.assert_array_equal(o["frame"], r["book_frame"].astype(np.int32))
     err = np.abs(o["obs"] - r["obs"])
-    assert (err <= 1e-6 + 2.0 ** -22 * np.abs(r["obs"])).all(), "obs beyond 1e-6 + 2 float32 ulps"
-    assert err.max() <= 1e-5
+    bound = 1e-6 + 2.0 ** -22 * np.abs(r["obs"])
+    # the fp32 state's base quaternion is rounded to float32 (half an ulp per component); the Euler angles
+    # (getEulerFromQuaternion: pitch = asin, roll / yaw = atan2 of terms that vanish at gimbal lock) amplify that
+    # by 1 / cos(pitch), and angle_to_target (obs 1, 2) inherits the yaw's error
+    cp = np.maximum(np.cos(r["obs"][:, 7].astype(np.float64)), 1e-3)
+    for k in (1, 2, 6, 7):
+        bound[:, k] += 2.0 ** -22 / cp
+    assert (err <= bound).all(), "obs beyond 1e-6 + 2 float32 ulps (+ the Euler angles' quaternion conditioning)"
+    assert (err[:, [0] + list(range(3, 6)) + list(range(8, 70))] <= 1e-5).all()
     np.testing.assert_allclose(o["rew"], r["reward"], rtol=0, atol=1e-4)
     np.testing.assert_allclose(o["book"][:, N.BK["target"]:N.BK["target"] + 3], r["book_target"], atol=1e-5)
     np.testing.assert_allclose(o["aux"][:, N.AUX.index("endPointScoreExp")], r["endpoint_score_exp"], atol=1e-5)
