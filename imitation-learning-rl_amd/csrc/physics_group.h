@@ -90,6 +90,24 @@ constexpr unsigned long long pack_bits(const int (&v)[N], int off = 0) {
 }
 __device__ inline int body_ndof_l(int b) { return (int)((pack_bits<2>(body_ndof) >> (2 * b)) & 3u); }
 __device__ inline int body_dof0_l(int b) { return (int)((pack_bits<5>(body_dof0) >> (5 * b)) & 31u); }
+// tree depth (torso 0) and parent (torso: itself) of each body, for lane-indexed lookups
+struct TreeInfo { int depth[NB], parent0[NB], maxdepth; };
+constexpr TreeInfo tree_info() {
+    TreeInfo t{};
+    t.maxdepth = 0;
+    for (int b = 0; b < NB; b++) {
+        int d = 0;
+        for (int y = b; y > 0; y = body_parent[y]) d++;
+        t.depth[b] = d;
+        t.parent0[b] = b > 0 ? body_parent[b] : 0;
+        t.maxdepth = d > t.maxdepth ? d : t.maxdepth;
+    }
+    return t;
+}
+constexpr TreeInfo TREE = tree_info();
+static_assert(TREE.maxdepth < 8 && NB <= 21, "3-bit depth codes");
+__device__ inline int body_depth_l(int b) { return (int)((pack_bits<3>(TREE.depth) >> (3 * b)) & 7u); }
+__device__ inline int body_parent_l(int b) { return (int)((pack_bits<4>(TREE.parent0) >> (4 * b)) & 15u); }
 struct LinkInfo { int nlink[NB], link0[NB]; };
 constexpr LinkInfo link_info() {
     LinkInfo r{};
@@ -1034,25 +1052,43 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     __syncthreads();
     PHASE(1);
+    // ---- body velocities root -> leaves, one tree depth per step (lane b = body b at that depth):
+    //      Vt[b] = Vt[parent] + sum over b's dofs of Sc * qd, the same additions in the same order as summing the
+    //      whole root path on every lane (4 short steps instead of 17 dofs of masked FMAs per lane).  Scratch:
+    //      the ABA's V slots, which pass 3 overwrites.
+    {
+        T* Vt = &S.x.aba.V[0][0];
+        if (l < 6) Vt[l] = S.nu[l];
+#pragma unroll
+        for (int lv = 1; lv <= TREE.maxdepth; lv++) {
+            wave_sync();
+            if (l < NB && body_depth_l(l) == lv) {
+                const int b = l, p = body_parent_l(b), k = body_ndof_l(b), d0 = body_dof0_l(b);
+                T v[6];
+#pragma unroll
+                for (int e = 0; e < 6; e++) v[e] = Vt[6 * p + e];
+                for (int j = 0; j < k; j++) {
+                    const int d = d0 + j;
+                    T Sc[6];
+                    load_sc(S, d, Sc);
+                    const T qd = S.nu[6 + d];
+#pragma unroll
+                    for (int e = 0; e < 6; e++) v[e] += Sc[e] * qd;
+                }
+#pragma unroll
+                for (int e = 0; e < 6; e++) Vt[6 * b + e] = v[e];
+            }
+        }
+        wave_sync();
+    }
     // ---- ABA pass 1: lane b = body b
     if (l < NB) {
         const int b = l;
         T V[6];
+        {   // parent velocity (the torso: the base velocity itself)
+            const int p = body_parent_l(b);
 #pragma unroll
-        for (int e = 0; e < 6; e++) V[e] = S.nu[e];
-        // parent velocity: path excluding b itself
-#pragma unroll
-        for (int x = 1; x < NB; x++) {
-            const bool on = on_path(x, b) && x != b;
-#pragma unroll
-            for (int k = 0; k < body_ndof[x]; k++) {
-                const int d = body_dof0[x] + k;
-                T Sc[6];
-                load_sc(S, d, Sc);
-                if (on)
-#pragma unroll
-                    for (int e = 0; e < 6; e++) V[e] += Sc[e] * S.nu[6 + d];
-            }
+            for (int e = 0; e < 6; e++) V[e] = S.x.aba.V[p][e];
         }
         SUBPHASE(13);
         T cb[6] = {0, 0, 0, 0, 0, 0};
