@@ -310,6 +310,14 @@ def main():
             env2.close()
             out["secondary"] = {other: {"value": n * 200 / w2, "ms_per_step": w2 / 200 * 1e3, "kernel_ms": k2,
                                         "steps": 200, "warmup": 20}}
+            if "split_penetration" not in phys:
+                # continuity with the bench lines measured before the split-impulse model:
+                # the same kernel on the previous workload (every limit / contact violation corrected at ERP)
+                prev = dict(phys, split_penetration=-1e30)
+                env3, w3, k3, _, _ = run(a, 1, 0, dev, n, a.precision, 200, 20, prev)
+                env3.close()
+                out["secondary"]["previous_model_split_off"] = {
+                    "value": n * 200 / w3, "ms_per_step": w3 / 200 * 1e3, "kernel_ms": k3, "steps": 200, "warmup": 20}
         if world == 1 and a.cpu_seconds > 0 and not a.hier:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_workers or host_cores())
         print(json.dumps(out), flush=True)

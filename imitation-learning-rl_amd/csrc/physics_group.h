@@ -268,8 +268,10 @@ __device__ inline void load_tab_lds() {   // block-wide; the caller's __syncthre
 // rows kept in LDS; rows beyond spill to a per-env global region and the wave takes the slow PGS path
 // (random-policy rollouts: p99 20 rows, > 30 in 0.04% of env-substeps; but the launch lasts as long as
 // its slowest wave, so a smaller capacity costs more than its frequency suggests: 24 rows is 9% slower)
+// 30 rows: 4 fp32 blocks of 4 envs take exactly the CU's 160 KB (29: 156.5 KB; 30 measured +0.3 % on the contact-rich
+// split-impulse workload, tools/gpu/ab.sh).  Diagnostic builds with extra shared memory use 29 (Makefile).
 #ifndef HUM_MAXR_LDS
-#define HUM_MAXR_LDS 29
+#define HUM_MAXR_LDS 30
 #endif
 constexpr int MAXR_LDS = HUM_MAXR_LDS;
 
@@ -292,6 +294,9 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
         } cr;
     } x;
 };
+
+static_assert(HUM_MAXR_LDS != 30 || 4 * sizeof(GroupLDS<float>) * 4 <= 160 * 1024,
+              "four blocks of four fp32 envs must fit one CU's LDS");
 
 template <typename T>
 __device__ __attribute__((always_inline)) inline void load_sc(const GroupLDS<T>& S, int d, T* Sc) {
