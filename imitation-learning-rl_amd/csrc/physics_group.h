@@ -26,7 +26,16 @@ constexpr int GL = 16;                       // lanes per env
 constexpr int MAXC_LDS = 16;
 constexpr int MAXC_G = MAXC;                 // = NCAND_ALL (physics.h)
 constexpr int CW = 12;                       // contact entry: ba, bb, pa[3], pb[3], n[3], d
-constexpr int MAXL_G = 2 * NDOF;             // limit rows (one per violated side)
+// limit rows: one per violated side, and a dof violates at most one side (lo < hi for every dof).  17 slots instead
+// of 34 also keep the per-env LDS stride off a multiple of 64 dwords (with 30 row slots, 34 made it exactly 2560
+// dwords: the 4 envs of a wave then hit the same LDS bank on every same-field access)
+constexpr int MAXL_G = NDOF;
+constexpr bool limits_proper() {
+    for (int d = 0; d < NDOF; d++)
+        if (!(dof_lo[d] < dof_hi[d])) return false;
+    return true;
+}
+static_assert(limits_proper(), "a dof with lo >= hi could violate both sides");
 constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // rows of one env: limits + (normal + 2 frictions) per contact
 // constraint row layout (T units): J and M^-1 J^T interleaved per dof ([2q] = J_q, [2q+1] = (M^-1 J^T)_q), a
 // zero pair (read by the lanes without a second velocity component), then two 16-byte scalar quads:
@@ -297,6 +306,7 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
 
 static_assert(HUM_MAXR_LDS != 30 || 4 * sizeof(GroupLDS<float>) * 4 <= 160 * 1024,
               "four blocks of four fp32 envs must fit one CU's LDS");
+static_assert((sizeof(GroupLDS<float>) / 4) % 64 != 0, "per-env LDS stride: not a multiple of the 64 banks");
 
 template <typename T>
 __device__ __attribute__((always_inline)) inline void load_sc(const GroupLDS<T>& S, int d, T* Sc) {
