@@ -2,12 +2,13 @@
 """Benchmark: env steps/s of the HIP humanoid imitation env (BASELINE.json metric).
 
 Workload (BASELINE.json configs[1]): 4096 lanes per GPU, low-level imitation on motion02_04, uniform
-random actions in [-1,1] (pre-generated pool, device resident), auto-reset of done lanes inside the
-step launch.  A "step" = one hum_step launch advancing every lane one env step (4 physics substeps +
-observation + imitation reward + bookkeeping).  Multi-GPU: one process per GPU, lanes sharded by rank
-(global lane ids -> identical per-lane streams regardless of N), no data-path collective -> weak scaling;
-`--gather-every K` adds the trajectory gather (RCCL all-gather of obs / action / reward / done every K steps,
-the only collective the path has), timed separately.
+random actions in [-1,1] (pre-generated pool, device resident, a fresh [n,17] action row for every env
+step), auto-reset of done lanes inside the launch.  A "step" = one env step of every lane (4 physics substeps +
+observation + imitation reward + bookkeeping); `--k K` env steps run per hum_step_k launch (outputs written
+per step, [K, n, ...]), and every rate below is per env-step.  Multi-GPU: one process per GPU, lanes sharded
+by rank (global lane ids -> identical per-lane streams regardless of N), no data-path collective -> weak
+scaling; `--gather-every G` adds the trajectory gather (ONE all-gather of the last G steps' obs / action /
+reward / done rows every G env steps, the only collective the path has), timed separately.
 
 Prints ONE JSON line on rank 0.  Every number in it is measured in this run except `roofline.traffic`
 (PMC bytes, profiles/pmc_traffic.json, from a rocprofv3 --pmc pass of this same command) and the static FLOP
@@ -30,6 +31,7 @@ BYTES_PER_STEP_LAYOUT = 2 * 47 * 4 + 2 * (23 * 8 + 8 * 4) + 17 * 4 + 70 * 4 + 4 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector
+K_DEFAULT = 8                  # env steps per launch (hum_step_k), DESIGN.md section 5
 
 
 def parse():
@@ -47,7 +49,13 @@ def parse():
     ap.add_argument("--phys", action="append", default=[], help="physics override k=v (hum_config field), diagnostics")
     ap.add_argument("--hier", action="store_true",
                     help="config 5: HierarchicalHumanoidEnv two-level rollout (hum_hier_step), clip motion09_03")
-    ap.add_argument("--gather-every", type=int, default=0, help="multi-GPU: trajectory all-gather every K steps")
+    ap.add_argument("--gather-every", type=int, default=0,
+                    help="multi-GPU: trajectory all-gather of the last G env steps every G env steps (G %% k == 0)")
+    ap.add_argument("--k", type=int, default=K_DEFAULT, help="env steps per launch (hum_step_k)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: host-staged, tests)")
+    ap.add_argument("--dump-gather", default=None,
+                    help="rank 0: save every gathered trajectory fragment to this .npz (tests)")
     ap.add_argument("--policy", action="store_true",
                     help="closed loop: actions from the on-GPU policy network (random-init weights, exploration "
                          "noise) inside the timed loop, SURVEY 8(f) rank 2")
@@ -149,25 +157,48 @@ def _load_json(path):
         return None
 
 
-def run(a, world, rank, dev, n, precision, steps, warmup, phys):
-    """Build the env, warm up, time `steps` launches.  Returns (env, wall_max_s, kernel_ms, low_steps)."""
+def _pools(a, dev, n, k, rank):
+    """16 device-resident action blocks [k, n, 17] (and [k, n, 2] high-level headings for --hier), a fresh row per
+    env step; launch s reads block s % 16."""
+    import torch
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = [(torch.rand(k, n, 17, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
+    hpool = [(torch.rand(k, n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)] if a.hier else None
+    return pool, hpool
+
+
+def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
+    """Build the env, warm up, time `steps` env steps in launches of k.  Returns (env, wall_max_s, kernel_ms per
+    env step, low_steps, gather_s, gathered)."""
     import torch
     import torch.distributed as dist
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    pool = [(torch.rand(n, 17, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
+    k = k or a.k
+    if a.policy:
+        k = 1   # closed loop: the policy acts on every step's observation
+    launches, wlaunches = -(-steps // k), -(-warmup // k)
+    pool, hpool = _pools(a, dev, n, k, rank)
+    G = a.gather_every
+    if G and G % k:
+        raise SystemExit("--gather-every must be a multiple of --k")
+    ring = [None] * (G // k if G else 1)   # output buffers of the launches since the last gather
     if a.hier:
         from ilrl_amd.hier_env import HierVecEnv
         env = HierVecEnv(n, seed=0, device=dev.index, lane_offset=rank * n, precision=precision, block_size=a.block,
                          **phys)
-        hpool = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
-        step = lambda s: env.step(hpool[s % 16], pool[s % 16], autoreset=True)
+
+        def step(s):
+            j = s % len(ring)
+            ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
     else:
         from ilrl_amd.clips import CLIP_NAMES
         from ilrl_amd.vec_env import HumanoidVecEnv
         clips = tuple(CLIP_NAMES) if a.clip == "all" else (a.clip,)
         env = HumanoidVecEnv(n, clips=clips, seed=0, device=dev.index, lane_offset=rank * n, precision=precision,
                              block_size=a.block, **phys)
-        step = lambda s: env.step(pool[s % 16], autoreset=True)
+
+        def step(s):
+            j = s % len(ring)
+            ring[j] = env.step_k(pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:
             from ilrl_amd.policy import DevicePolicy
             pol = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
@@ -178,61 +209,80 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys):
                 return env.step(actbuf, autoreset=True)
     env.reset()
     env.done.zero_()
-    for w in range(warmup):
+    for w in range(wlaunches):
         step(w)
-    gather_s = 0.0
+    gather_s, gathered = 0.0, []
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
-    for s in range(steps):
+    ev0.record(stream)
+    for s in range(launches):
         step(s)
-        if a.gather_every and world > 1 and (s + 1) % a.gather_every == 0:
-            from ilrl_amd.parallel import gather_trajectories
+        if G and world > 1 and not a.policy and ((s + 1) * k) % G == 0:
             tg = time.perf_counter()
-            gather_trajectories([env.obs, pool[s % 16], env.reward, env.done], dst=0)
+            frag = _fragment(a, ring, [pool[(s - j) % 16] for j in range(len(ring) - 1, -1, -1)])
+            from ilrl_amd.parallel import gather_trajectories
+            got = gather_trajectories(frag, dst=0)
+            if got is not None and a.dump_gather:
+                gathered.append([x.cpu() for x in got])
             gather_s += time.perf_counter() - tg
-    ev1.record()
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / steps   # average launch duration on the launch stream (torch's current)
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    kern_ms = ev0.elapsed_time(ev1) / (launches * k)   # per env step, on the launch stream (torch's current)
+    wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if world > 1 else wall
     low_steps = None
     if a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
-        lt = torch.tensor([count_hier_low_steps(a, dev, n, precision, steps, warmup, phys, rank)], dtype=torch.float64,
-                          device=dev)
+        low_steps = float(count_hier_low_steps(a, dev, n, precision, launches, wlaunches, k, phys, rank))
         if world > 1:
-            dist.all_reduce(lt)
-        low_steps = float(lt.item())   # all ranks
-    return env, float(t.item()), kern_ms, low_steps, gather_s
+            low_steps = _all_reduce(world, dev, a.backend, low_steps, dist.ReduceOp.SUM)   # all ranks
+    return env, wall, kern_ms, low_steps, gather_s, gathered
 
 
-def count_hier_low_steps(a, dev, n, precision, steps, warmup, phys, rank):
-    """Lanes that take a low-level (physics) step in each of the timed launches: a lane acts high next iff its
-    last outputs carried the high-level obs (level hand-back, or done -> auto-reset)."""
+def _all_reduce(world, dev, backend, x, op):
+    """One float reduced over the ranks (a host tensor for gloo, a device tensor for RCCL)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def _fragment(a, ring, acts):
+    """The last G env steps as lane-major buffers [n, G, ...] for the gather: obs, action, reward, done (hier: the
+    low-level obs / action / reward and done of every transition)."""
+    import torch
+    cat = lambda xs: torch.cat(xs, dim=0).transpose(0, 1).contiguous()
+    if a.hier:
+        return [cat([r[2] for r in ring]), cat(acts), cat([r[4] for r in ring]), cat([r[5] for r in ring])]
+    return [cat([r[0] for r in ring]), cat(acts), cat([r[1] for r in ring]), cat([r[2] for r in ring])]
+
+
+def count_hier_low_steps(a, dev, n, precision, launches, wlaunches, k, phys, rank):
+    """Lanes that take a low-level (physics) step in each transition of the timed launches: a lane acts high next
+    iff its last outputs carried the high-level obs (level hand-back, or done -> auto-reset)."""
     import torch
     from ilrl_amd import _native as N
     from ilrl_amd.hier_env import HierVecEnv
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    pool = [(torch.rand(n, 17, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
-    hpool = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(16)]
+    pool, hpool = _pools(a, dev, n, k, rank)
     env = HierVecEnv(n, seed=0, device=dev.index, lane_offset=rank * n, precision=precision, block_size=a.block, **phys)
     env.reset()
     expect_high = torch.ones(n, dtype=torch.bool, device=dev)
-    low = 0
-    for s in range(warmup + steps):
-        if s >= warmup:
-            low += int((~expect_high).sum().item())
-        agents, _, _, _, _, done, _ = env.step(hpool[s % 16], pool[s % 16], autoreset=True)
-        expect_high = ((agents & N.HUM_AGENT_HIGH) != 0) | (done != 0)
+    low, out = 0, None
+    for s in range(wlaunches + launches):
+        out = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=out)
+        agents, done = out[0], out[5]
+        for t in range(k):
+            if s >= wlaunches:
+                low += int((~expect_high).sum().item())
+            expect_high = ((agents[t] & N.HUM_AGENT_HIGH) != 0) | (done[t] != 0)
     env.close()
     return low
 
@@ -244,32 +294,48 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible devices share them (tests on a one-GPU box)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     n = a.lanes
     phys = {}
     for kv in a.phys:
-        k, v = kv.split("=")
-        phys[k] = float(v) if "." in v else int(v)
+        key, v = kv.split("=")
+        phys[key] = float(v) if "." in v else int(v)
     if a.hier:
         from ilrl_amd.hier_env import HIER_CLIP
         a.clip = HIER_CLIP
-    env, wall_max, kern_ms, low_steps, gather_s = run(a, world, rank, dev, n, a.precision, a.steps, a.warmup, phys)
+    if a.policy:
+        a.k = 1
+    if a.k < 1:
+        raise SystemExit("--k must be >= 1")
+    a.steps = -(-a.steps // a.k) * a.k      # whole launches
+    a.warmup = -(-a.warmup // a.k) * a.k
+    env, wall_max, kern_ms, low_steps, gather_s, gathered = run(a, world, rank, dev, n, a.precision, a.steps, a.warmup,
+                                                                phys)
     flags = env.error_flags()
+    if rank == 0 and a.dump_gather and gathered:
+        import numpy as np
+        names = ("obs", "act", "reward", "done")
+        np.savez(a.dump_gather, **{"%s_%d" % (nm, j): g[c].numpy() for j, g in enumerate(gathered)
+                                   for c, nm in enumerate(names)})
     if rank == 0:
         total = n * world * a.steps
-        phys_steps_per_launch = (low_steps / world / a.steps) if a.hier else n   # per GPU
+        phys_steps_per_step = (low_steps / world / a.steps) if a.hier else n   # per GPU, per env step
         value = (low_steps if a.hier else total) / wall_max
         flops_j = _load_json("profiles/r02_flops_per_env_step.json")
         flops = flops_j["flops_per_env_step_mean"] if flops_j else None
-        achieved = phys_steps_per_launch * BYTES_PER_STEP_ALGO / (kern_ms * 1e-3) / 1e9
+        achieved = phys_steps_per_step * BYTES_PER_STEP_ALGO / (kern_ms * 1e-3) / 1e9
         traffic = None
         tj = _load_json("profiles/pmc_traffic.json") or {}
-        key = "%s_%d_%s" % ("hier" if a.hier else a.clip, n, a.precision)
-        if key in tj:
-            traffic = tj[key]["bytes_per_launch"]
+        tkey = "%s_%d_%s_k%d" % ("hier" if a.hier else a.clip, n, a.precision, a.k)
+        if tkey in tj:
+            traffic = tj[tkey]["bytes_per_env_step"] * phys_steps_per_step
         out = {
             "metric": "env steps/sec at N parallel humanoids, 1/2/4/8 MI355X; obs/reward max-abs-err vs PyBullet",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -277,47 +343,51 @@ def main():
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
             "config": {"workload": ("HumanoidBulletEnv-v0-Hier two-level rollout (high heading every 5 low steps), "
                                     if a.hier else "HumanoidBulletEnv-v0-Low step+reward, ") +
-                                   "%s, %d envs/GPU, %s, auto-reset" % (
+                                   "%s, %d envs/GPU, %s, auto-reset, %d env steps per launch" % (
                                        a.clip, n, "on-GPU policy actions (random-init 70-256-256-17 tanh MLP + "
-                                       "Gaussian exploration) in the loop" if a.policy else "uniform random actions"),
-                       "envs_per_gpu": n, "clip": a.clip,
+                                       "Gaussian exploration) in the loop" if a.policy else
+                                       "uniform random actions (a fresh row per env step)", a.k),
+                       "envs_per_gpu": n, "clip": a.clip, "steps_per_launch": a.k,
                        "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
+            # per env step: kernel_ms = launch duration / k; achieved = the env step's algorithmic bytes over it
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per env step of all lanes (PMC, profiles/pmc_traffic.json)",
                          "bytes_per_env_step": BYTES_PER_STEP_ALGO, "bytes_per_env_step_layout": BYTES_PER_STEP_LAYOUT,
-                         "kernel_ms": kern_ms},
+                         "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * a.k},
             "error_flags": flags,
         }
         if flops:
             peak = FP32_PEAK_TFLOPS if a.precision == "fp32" else FP64_PEAK_TFLOPS
-            tf = phys_steps_per_launch * flops / (kern_ms * 1e-3) / 1e12
+            tf = phys_steps_per_step * flops / (kern_ms * 1e-3) / 1e12
             out["roofline_valu"] = {"bound": "valu-%s" % a.precision, "achieved": tf, "peak": peak, "unit": "TFLOP/s",
                                     "frac": tf / peak, "flops_per_env_step": flops,
                                     "source": "profiles/r02_flops_per_env_step.json (tools/flop_count.py)"}
         if a.hier:
             out["unit"] = "env-steps/s"
-            out["physics_env_steps_per_launch"] = phys_steps_per_launch
+            out["physics_env_steps_per_step"] = phys_steps_per_step
             out["agent_transitions_per_s"] = total / wall_max
         if world > 1 and a.gather_every:
-            out["gather"] = {"every": a.gather_every, "seconds": gather_s,
-                             "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1)}
+            out["gather"] = {"every": a.gather_every, "seconds": gather_s, "backend": a.backend,
+                             "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1), "fragments": len(gathered) or None}
         if world == 1 and not a.no_secondary and not a.hier and not a.policy:
             from ilrl_amd.clips import CLIP_NAMES
             clips = tuple(CLIP_NAMES) if a.clip == "all" else (a.clip,)
             out["parity"] = parity_sample(env, clips)
+            sec = {}
             other = "fp64" if a.precision == "fp32" else "fp32"
-            env2, w2, k2, _, _ = run(a, 1, 0, dev, n, other, 200, 20, phys)
-            env2.close()
-            out["secondary"] = {other: {"value": n * 200 / w2, "ms_per_step": w2 / 200 * 1e3, "kernel_ms": k2,
-                                        "steps": 200, "warmup": 20}}
+            runs = [(other, other, phys, a.k), ("k1", a.precision, phys, 1)]
             if "split_penetration" not in phys:
                 # continuity with the bench lines measured before the split-impulse model:
                 # the same kernel on the previous workload (every limit / contact violation corrected at ERP)
-                prev = dict(phys, split_penetration=-1e30)
-                env3, w3, k3, _, _ = run(a, 1, 0, dev, n, a.precision, 200, 20, prev)
-                env3.close()
-                out["secondary"]["previous_model_split_off"] = {
-                    "value": n * 200 / w3, "ms_per_step": w3 / 200 * 1e3, "kernel_ms": k3, "steps": 200, "warmup": 20}
+                runs.append(("previous_model_split_off", a.precision, dict(phys, split_penetration=-1e30), a.k))
+            for name, prec, ph, kk in runs:
+                st, wu = 200, 24
+                e2, w2, k2, _, _, _ = run(a, 1, 0, dev, n, prec, st, wu, ph, k=kk)
+                e2.close()
+                sec[name] = {"value": n * st / w2, "ms_per_step": w2 / st * 1e3, "kernel_ms": k2, "steps": st,
+                             "warmup": wu, "steps_per_launch": kk, "precision": prec}
+            out["secondary"] = sec
         if world == 1 and a.cpu_seconds > 0 and not a.hier:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_workers or host_cores())
         print(json.dumps(out), flush=True)

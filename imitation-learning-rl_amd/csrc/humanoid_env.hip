@@ -54,6 +54,8 @@ struct hum_env {
     float* hf;
     int hf_w, hf_l;
     double hf_s[3], hf_o[3], hf_mid;
+    void* stage;          // HUM_STEP_HOST_IO: device staging for host buffers (grown on demand)
+    size_t stage_bytes;
     hipGraphExec_t graph;
     int graph_k;
     const void* graph_key[6];
@@ -109,6 +111,7 @@ KArgs make_args(hum_env* e) {
     a.bd = e->d.bd;
     a.scratch = e->d.scratch;
     a.eflags = e->eflags;
+    a.ksteps = 1;
     return a;
 }
 dim3 grid_of(hum_env* e) { return dim3((e->n + e->cfg.block_size - 1) / e->cfg.block_size); }
@@ -243,6 +246,7 @@ int hum_destroy(hum_env* e) {
     (void)hipFree(e->clips_dev);
     (void)hipFree(e->pred);
     (void)hipFree(e->hf);
+    (void)hipFree(e->stage);
     for (int k = 0; k < HUM_MAX_CLIPS; k++) (void)hipFree(e->clip_dev[k]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -305,6 +309,11 @@ int hum_set_predefined_targets(hum_env* e, const double* xyz, int32_t n) {
 
 int hum_set_terrain(hum_env* e, int32_t mode, const float* heights, int32_t w, int32_t l, const double* scale3,
                     const double* origin3) {
+    return hum_set_terrain_ex(e, mode, heights, w, l, scale3, origin3, nullptr);
+}
+
+int hum_set_terrain_ex(hum_env* e, int32_t mode, const float* heights, int32_t w, int32_t l, const double* scale3,
+                       const double* origin3, const double* centre) {
     if (!e) return fail(HUM_ERR_ARG, "hum_set_terrain: null env");
     if (mode != HUM_TERRAIN_PLANE && mode != HUM_TERRAIN_HEIGHTFIELD && mode != HUM_TERRAIN_RANDOM_BLOCKS)
         return fail(HUM_ERR_ARG, "hum_set_terrain: unknown mode");
@@ -316,8 +325,8 @@ int hum_set_terrain(hum_env* e, int32_t mode, const float* heights, int32_t w, i
     int W = 256, L = 256;
     if (mode == HUM_TERRAIN_HEIGHTFIELD) {
         if (!heights || !scale3 || !origin3 || w < 2 || l < 2) return fail(HUM_ERR_ARG, "hum_set_terrain: bad heightfield");
-        if (!(scale3[0] >= 0.5 && scale3[1] >= 0.5 && scale3[2] > 0))
-            return fail(HUM_ERR_ARG, "hum_set_terrain: scale x, y must be >= 0.5 and z > 0");
+        if (!(scale3[0] >= 0.25 && scale3[1] >= 0.25 && scale3[2] > 0))
+            return fail(HUM_ERR_ARG, "hum_set_terrain: scale x, y must be >= 0.25 and z > 0");
         W = w;
         L = l;
         h.assign(heights, heights + (size_t)w * l);
@@ -327,7 +336,10 @@ int hum_set_terrain(hum_env* e, int32_t mode, const float* heights, int32_t w, i
             lo = v < lo ? v : lo;
             hi = v > hi ? v : hi;
         }
-        mid = 0.5 * ((double)lo + (double)hi);   // btHeightfieldTerrainShape m_localOrigin
+        // btHeightfieldTerrainShape m_localOrigin: the (min + max) / 2 of the data the shape was CREATED with; a
+        // replaceHeightfieldIndex update (CustomScene.replaceHeightfieldData) keeps the creation value (centre)
+        mid = centre ? *centre : 0.5 * ((double)lo + (double)hi);
+        if (!std::isfinite(mid)) return fail(HUM_ERR_ARG, "hum_set_terrain: non-finite centre");
         for (int k = 0; k < 3; k++) { s[k] = scale3[k]; o[k] = origin3[k]; }
     }
     HIPCHK(hipSetDevice(e->cfg.device));
@@ -371,9 +383,74 @@ int hum_reset_ex(hum_env* e, const uint8_t* lane_mask, const int32_t* start_fram
     return HUM_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// HUM_STEP_HOST_IO: the hot-path buffers are host pointers.  Stage them through one device allocation on the launch
+// stream (inputs and outputs copied in - outputs too, so rows a step leaves unwritten keep the caller's values -, the
+// launch, outputs copied back), then synchronise.  bufs[j].p points at the argument slot, rewritten to the staging
+// address for the launch.
+struct HostBuf { const void** p; size_t bytes; bool out; };
+template <typename F>
+int staged(hum_env* e, hipStream_t s, HostBuf* bufs, int nb, F launch) {
+    size_t total = 0;
+    for (int j = 0; j < nb; j++)
+        if (*bufs[j].p) total += (bufs[j].bytes + 255) / 256 * 256;
+    if (total > e->stage_bytes) {
+        HIPCHK(hipStreamSynchronize(s));
+        if (e->stage) HIPCHK(hipFree(e->stage));
+        e->stage = nullptr;
+        e->stage_bytes = 0;
+        HIPCHK(hipMalloc(&e->stage, total));
+        e->stage_bytes = total;
+    }
+    const void* host[16];
+    size_t off = 0;
+    for (int j = 0; j < nb; j++) {
+        host[j] = *bufs[j].p;
+        if (!host[j]) continue;
+        void* d = (char*)e->stage + off;
+        off += (bufs[j].bytes + 255) / 256 * 256;
+        HIPCHK(hipMemcpyAsync(d, host[j], bufs[j].bytes, hipMemcpyHostToDevice, s));
+        *bufs[j].p = d;
+    }
+    const int rc = launch();
+    for (int j = 0; j < nb; j++) {
+        if (host[j] && bufs[j].out && rc == HUM_OK)
+            HIPCHK(hipMemcpyAsync(const_cast<void*>(host[j]), *bufs[j].p, bufs[j].bytes, hipMemcpyDeviceToHost, s));
+        *bufs[j].p = host[j];
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return rc;
+}
+// HUM_STEP_CHECK_FINITE: wait for the launch and turn a non-finite action (humanoid.py:55 assert) into an error
+// status; the bit is taken out of the sticky flags
+int check_finite(hum_env* e, hipStream_t s) {
+    unsigned v = 0;
+    HIPCHK(hipMemcpyAsync(&v, e->eflags, sizeof v, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!(v & HUM_EFLAG_NONFINITE_ACTION)) return HUM_OK;
+    const unsigned w = v & ~HUM_EFLAG_NONFINITE_ACTION;
+    HIPCHK(hipMemcpyAsync(e->eflags, &w, sizeof w, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return fail(HUM_ERR_ARG, "hum_step: non-finite action (humanoid.py:55 assert np.isfinite(a).all()): those lanes "
+                             "were not stepped");
+}
+constexpr uint32_t STEP_FLAGS = HUM_STEP_AUTORESET | HUM_STEP_SKIP_PHYSICS | HUM_STEP_HOST_IO | HUM_STEP_CHECK_FINITE;
+}  // namespace
+
+extern "C" {
+
 int hum_step(hum_env* e, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
              uint32_t flags, float* obs_reset, void* stream) {
+    return hum_step_k(e, actions, obs, reward, done, frame, flags, obs_reset, 1, stream);
+}
+
+int hum_step_k(hum_env* e, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
+               uint32_t flags, float* obs_reset, int32_t k, void* stream) {
     if (!e || !actions || !obs || !reward || !done) return fail(HUM_ERR_ARG, "hum_step: null argument");
+    if (k < 1) return fail(HUM_ERR_ARG, "hum_step_k: k must be >= 1");
+    if (flags & ~STEP_FLAGS) return fail(HUM_ERR_ARG, "hum_step: unknown flags");
     if (e->cfg.hier) return fail(HUM_ERR_STATE, "hum_step: hierarchical handle (use hum_hier_step)");
     if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_step: no clip uploaded (hum_set_clip)");
     HIPCHK(hipSetDevice(e->cfg.device));
@@ -383,9 +460,22 @@ int hum_step(hum_env* e, const float* actions, float* obs, float* reward, uint8_
     a.rew = reward;
     a.done = done;
     a.frame_out = frame;
-    a.flags = flags;
+    a.flags = flags & (HUM_STEP_AUTORESET | HUM_STEP_SKIP_PHYSICS);
     a.obs_reset = obs_reset;
-    return launch_step(e, a, stream_of(e, stream));
+    a.ksteps = k;
+    const hipStream_t s = stream_of(e, stream);
+    int rc;
+    if (flags & HUM_STEP_HOST_IO) {
+        const size_t kn = (size_t)k * e->n;
+        HostBuf b[6] = {{(const void**)&a.act, kn * HUM_NACT * 4, false}, {(const void**)&a.obs, kn * HUM_NOBS * 4, true},
+                        {(const void**)&a.rew, kn * 4, true}, {(const void**)&a.done, kn, true},
+                        {(const void**)&a.frame_out, kn * 4, true}, {(const void**)&a.obs_reset, kn * HUM_NOBS * 4, true}};
+        rc = staged(e, s, b, 6, [&] { return launch_step(e, a, s); });
+    } else {
+        rc = launch_step(e, a, s);
+    }
+    if (rc == HUM_OK && (flags & HUM_STEP_CHECK_FINITE)) rc = check_finite(e, s);
+    return rc;
 }
 
 int hum_hier_reset(hum_env* e, const uint8_t* lane_mask, const int32_t* start_frame, const double* reset_yaw_deg,
@@ -416,8 +506,17 @@ int hum_hier_reset_ex(hum_env* e, const uint8_t* lane_mask, const int32_t* start
 int hum_hier_step(hum_env* e, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
                   float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
                   uint32_t flags, float* high_obs_reset, void* stream) {
+    return hum_hier_step_k(e, high_act, low_act, agent, agents, high_obs, low_obs, high_rew, low_rew, done, frame, flags,
+                           high_obs_reset, 1, stream);
+}
+
+int hum_hier_step_k(hum_env* e, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
+                    float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
+                    uint32_t flags, float* high_obs_reset, int32_t k, void* stream) {
     if (!e || !high_act || !low_act || !agents || !high_obs || !low_obs || !high_rew || !low_rew || !done)
         return fail(HUM_ERR_ARG, "hum_hier_step: null argument");
+    if (k < 1) return fail(HUM_ERR_ARG, "hum_hier_step_k: k must be >= 1");
+    if (flags & ~STEP_FLAGS) return fail(HUM_ERR_ARG, "hum_hier_step: unknown flags");
     if (!e->cfg.hier) return fail(HUM_ERR_STATE, "hum_hier_step: handle was not created with hier = 1");
     if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_hier_step: no clip uploaded (hum_set_clip)");
     HIPCHK(hipSetDevice(e->cfg.device));
@@ -432,9 +531,27 @@ int hum_hier_step(hum_env* e, const float* high_act, const float* low_act, const
     a.rew_high = high_rew;
     a.done = done;
     a.frame_out = frame;
-    a.flags = flags;
+    a.flags = flags & (HUM_STEP_AUTORESET | HUM_STEP_SKIP_PHYSICS);
     a.obs_high_reset = high_obs_reset;
-    return launch_step(e, a, stream_of(e, stream));
+    a.ksteps = k;
+    const hipStream_t s = stream_of(e, stream);
+    int rc;
+    if (flags & HUM_STEP_HOST_IO) {
+        const size_t kn = (size_t)k * e->n;
+        HostBuf b[12] = {{(const void**)&a.act, kn * HUM_NACT * 4, false},
+                         {(const void**)&a.act_high, kn * HUM_NACT_HIGH * 4, false},
+                         {(const void**)&a.agent_sel, kn, false}, {(const void**)&a.agents, kn, true},
+                         {(const void**)&a.obs_high, kn * HUM_NOBS_HIGH * 4, true},
+                         {(const void**)&a.obs, kn * HUM_NOBS * 4, true}, {(const void**)&a.rew_high, kn * 4, true},
+                         {(const void**)&a.rew, kn * 4, true}, {(const void**)&a.done, kn, true},
+                         {(const void**)&a.frame_out, kn * 4, true},
+                         {(const void**)&a.obs_high_reset, kn * HUM_NOBS_HIGH * 4, true}, {nullptr, 0, false}};
+        rc = staged(e, s, b, 11, [&] { return launch_step(e, a, s); });
+    } else {
+        rc = launch_step(e, a, s);
+    }
+    if (rc == HUM_OK && (flags & HUM_STEP_CHECK_FINITE)) rc = check_finite(e, s);
+    return rc;
 }
 
 }  // extern "C"
@@ -486,6 +603,8 @@ extern "C" {
 int hum_step_graph(hum_env* e, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
                    uint32_t flags, float* obs_reset, int32_t k) {
     if (!e || k <= 0) return fail(HUM_ERR_ARG, "hum_step_graph: bad argument");
+    if (flags & (HUM_STEP_HOST_IO | HUM_STEP_CHECK_FINITE))
+        return fail(HUM_ERR_ARG, "hum_step_graph: HUM_STEP_HOST_IO / HUM_STEP_CHECK_FINITE synchronise (not capturable)");
     HIPCHK(hipSetDevice(e->cfg.device));
     const void* key[6] = {actions, obs, reward, done, frame, obs_reset};
     bool same = e->graph && e->graph_k == k && e->graph_flags == flags && memcmp(key, e->graph_key, sizeof key) == 0;
@@ -689,6 +808,10 @@ int hum_sync(hum_env* e) {
 }
 
 int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
+
+}  // extern "C"
+__attribute__((visibility("hidden"))) int hum_internal_device(const hum_env* e) { return e ? e->cfg.device : -1; }
+extern "C" {
 
 
 #ifdef HUM_WLOG_ON

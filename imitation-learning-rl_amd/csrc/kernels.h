@@ -65,7 +65,31 @@ struct KArgs {
     float* obs_high;                // [n,44]
     float* rew_high;                // [n]
     float* obs_high_reset;          // [n,44]
+    // multi-step launch (hum_step_k / hum_hier_step_k): env steps per launch; the per-step inputs and outputs
+    // above are then [ksteps, n, ...] arrays, step-major (step t at offset t * n * width)
+    int ksteps;
 };
+
+// the inputs / outputs of step t of a multi-step launch (NULL stays NULL)
+__device__ inline KArgs step_args(const KArgs& a, int t) {
+    if (t == 0) return a;
+    KArgs s = a;
+    const long o = (long)t * a.n;
+    auto off = [o](auto* p, int w) { return p ? p + o * w : p; };
+    s.act = off(a.act, HUM_NACT);
+    s.obs = off(a.obs, HUM_NOBS);
+    s.rew = off(a.rew, 1);
+    s.done = off(a.done, 1);
+    s.frame_out = off(a.frame_out, 1);
+    s.obs_reset = off(a.obs_reset, HUM_NOBS);
+    s.act_high = off(a.act_high, HUM_NACT_HIGH);
+    s.agent_sel = off(a.agent_sel, 1);
+    s.agents = off(a.agents, 1);
+    s.obs_high = off(a.obs_high, HUM_NOBS_HIGH);
+    s.rew_high = off(a.rew_high, 1);
+    s.obs_high_reset = off(a.obs_high_reset, HUM_NOBS_HIGH);
+    return s;
+}
 
 // CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
 // np.clip(a, -1, 1)) - a float32 product under NumPy >= 2 (NEP 50), float64 under NumPy 1.x
@@ -584,46 +608,51 @@ __device__ inline void nonfinite_outputs(const KArgs& a, int i, int frame) {
 
 // ----------------------------------------------------------------------------------- step
 template <typename T>
-__global__ void __launch_bounds__(256) step_kernel(KArgs a) {
+__global__ void __launch_bounds__(256) step_kernel(KArgs a0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+    if (i >= a0.n) return;
     T st[HUM_NSTATE];
     Book b;
-    load_lane(a, i, st, b);
+    load_lane(a0, i, st, b);
     unsigned ef = 0;
-    // hierarchical env: the lane's acting agent (step(action_dict) dispatch, hier_env.py:363-366); a lane with
-    // no action this round (HUM_AGENT_SEL_SKIP) is left untouched and reports no agent
-    if (a.hier && a.agent_sel && a.agent_sel[i] == HUM_AGENT_SEL_SKIP) {
-        a.agents[i] = 0;
-        return;
-    }
-    const bool high = a.hier && (a.agent_sel ? a.agent_sel[i] != 0 : b.expect_high != 0);
-    float act[HUM_NACT];
-    bool finite = true;
-#pragma unroll
-    for (int k = 0; k < HUM_NACT; k++) {
-        act[k] = a.act[(long)i * HUM_NACT + k];
-        finite &= isfinite(act[k]);
-    }
-    if (!finite && !high) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
-        ef |= HUM_EFLAG_NONFINITE_ACTION;
-        nonfinite_outputs(a, i, b.frame);
-        atomicOr(a.eflags, ef);
-        return;
-    }
-    if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && !high) {
-        T tau[NDOF];
-#pragma unroll
-        for (int k = 0; k < HUM_NACT; k++)   // apply_action
-            tau[act_dof[k]] = (T)motor_torque(a.np1, (float)act_gain[k], act_gain[k], act[k]);
-        Lane<T> rows{(T*)a.scratch + i, (long)a.n};
 #pragma unroll 1
-        for (int s = 0; s < a.P.nsub; s++) {
-            if (substep(a.P, st, tau, rows)) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
+    for (int t = 0; t < a0.ksteps; t++) {   // env steps of this launch (state and book stay in registers)
+        const KArgs a = step_args(a0, t);
+        // hierarchical env: the lane's acting agent (step(action_dict) dispatch, hier_env.py:363-366); a lane with
+        // no action this round (HUM_AGENT_SEL_SKIP) is left untouched and reports no agent
+        if (a.hier && a.agent_sel && a.agent_sel[i] == HUM_AGENT_SEL_SKIP) {
+            a.agents[i] = 0;
+            continue;
         }
+        const bool high = a.hier && (a.agent_sel ? a.agent_sel[i] != 0 : b.expect_high != 0);
+        float act[HUM_NACT];
+        bool finite = true;
+#pragma unroll
+        for (int k = 0; k < HUM_NACT; k++) {
+            act[k] = a.act[(long)i * HUM_NACT + k];
+            finite &= isfinite(act[k]);
+        }
+        if (!finite && !high) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
+            ef |= HUM_EFLAG_NONFINITE_ACTION;
+            nonfinite_outputs(a, i, b.frame);
+            continue;
+        }
+        if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && !high) {
+            T tau[NDOF];
+#pragma unroll
+            for (int k = 0; k < HUM_NACT; k++)   // apply_action
+                tau[act_dof[k]] = (T)motor_torque(a.np1, (float)act_gain[k], act_gain[k], act[k]);
+            Lane<T> rows{(T*)a.scratch + i, (long)a.n};
+#pragma unroll 1
+            for (int s = 0; s < a.P.nsub; s++) {
+                if (substep(a.P, st, tau, rows)) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
+            }
+        }
+        unsigned ef1 = 0;   // hier_post / post_step publish their own flags
+        if (a.hier) hier_post(a, i, st, b, high, ef1);
+        else post_step(a, i, st, b, act, ef1);
     }
-    if (a.hier) hier_post(a, i, st, b, high, ef);
-    else post_step(a, i, st, b, act, ef);
+    if (ef) atomicOr(a0.eflags, ef);
 }
 
 // Cooperative step: 16 lanes per env, EPB_ envs per block of EPB_*16 threads (one wavefront), env working
@@ -633,7 +662,7 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
 #define HUM_GROUP_MIN_WAVES 1
 #endif
 template <typename T, int EPB_, bool TERRAIN = false>
-__global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a) {
+__global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a0) {
     __shared__ GroupLDS<T> sh[EPB_];
     const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
     // XCD-aware env mapping: the dispatcher deals blocks round-robin over the 8 XCDs (block b -> XCD b % 8),
@@ -642,7 +671,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     const int nb = gridDim.x, xq = nb >> 3, xr = nb & 7, xcd = blockIdx.x & 7;
     const int blk = xcd * xq + min(xcd, xr) + (blockIdx.x >> 3);
     const int i = blk * EPB_ + ge;
-    const bool valid = i < a.n;
+    const bool valid = i < a0.n;
     GroupLDS<T>& S = sh[ge];
 #ifdef HUM_WLOG_ON
     const unsigned long long t_wave0 = __builtin_amdgcn_s_memtime();
@@ -652,28 +681,40 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
 #endif
 #endif
     load_tab_lds<T>();
-    __syncthreads();
     const ModelTab<T>& M = tab<T>();
+    // the env's state stays in LDS over the steps of the launch; lane 0 carries the per-env integers the other
+    // lanes read (the agent the hierarchical env expects, the random-terrain key) in the pad slots of tau
     for (int e = l; e < HUM_NSTATE; e += GL)
-        S.st[e] = valid ? ((const T*)a.phys)[(long)e * a.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
+        S.st[e] = valid ? ((const T*)a0.phys)[(long)e * a0.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
+    static_assert(sizeof(T) * 3 >= 3 * sizeof(int), "carry slots");
+    int* carry = reinterpret_cast<int*>(&S.tau[NDOF]);
+    if (l == 0) {
+        carry[0] = valid && a0.hier ? a0.bi[10 * a0.n + i] : 0;
+        carry[1] = TERRAIN && a0.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid ? a0.bi[11 * a0.n + i] : 0;
+        carry[2] = TERRAIN && a0.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid ? a0.bi[12 * a0.n + i] : 0;
+    }
+    __syncthreads();
+    unsigned ef = 0;
+    const int gbit = (threadIdx.x & 63) & ~(GL - 1);
+#pragma unroll 1
+    for (int t = 0; t < a0.ksteps; t++) {
+    const KArgs a = step_args(a0, t);
     bool fin = true;
     for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60)
         const float av = valid ? a.act[(long)i * HUM_NACT + k] : 0.f;
         fin = fin && isfinite(av);
         S.tau[M.act_dof[k]] = (T)motor_torque(a.np1, M.act_gain[k], M.act_gain_d[k], isfinite(av) ? av : 0.f);
     }
-    const int gbit = (threadIdx.x & 63) & ~(GL - 1);
     // hierarchical env: envs whose acting agent is the high level take no physics step (hier_env.py:538-571)
     const unsigned char sel = a.hier && valid && a.agent_sel ? a.agent_sel[i] : (unsigned char)0;
     const bool skip = a.hier && valid && a.agent_sel && sel == HUM_AGENT_SEL_SKIP;   // no action: lane untouched
-    const bool high = a.hier && valid && !skip && (a.agent_sel ? sel != 0 : a.bi[10 * a.n + i] != 0);
+    const bool high = a.hier && valid && !skip && (a.agent_sel ? sel != 0 : carry[0] != 0);
     const bool env_ok = high || ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
     const bool any_phys = __ballot(valid && !high && !skip) != 0;   // wave-uniform
-    __syncthreads();
-    unsigned ef = 0;
     // the env's terrain (HUM_TERRAIN_RANDOM_BLOCKS: drawn at its last reset)
     const unsigned long long tkey = TERRAIN && a.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid
-        ? ((unsigned long long)(unsigned)a.bi[11 * a.n + i] | ((unsigned long long)(unsigned)a.bi[12 * a.n + i] << 32)) : 0ull;
+        ? ((unsigned long long)(unsigned)carry[1] | ((unsigned long long)(unsigned)carry[2] << 32)) : 0ull;
+    __syncthreads();
     if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && any_phys) {
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++)
@@ -692,7 +733,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     PHASE_INIT;
     Book b;
     T st[HUM_NSTATE];
-    bool rst = false;
+    bool rst = false, stored = false;
     if (valid && l == 0 && skip) {
         a.agents[i] = 0;
     } else if (valid && l == 0) {
@@ -711,6 +752,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             }
             if (a.hier) {
                 hier_post(a, i, st, b, high, ef, high ? nullptr : scs);   // high: the HBM state, not S.st
+                stored = true;
             } else {
                 float act[HUM_NACT];
 #pragma unroll
@@ -759,9 +801,26 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
                 }
             }
             store_lane(a, i, st, b);
+            stored = true;
         }
     }
     PHASE(10);
+    if (a0.ksteps > 1) {   // wave-uniform: publish the env's state for the next step of this launch
+        if (valid && l == 0) {
+            if (!stored) {   // not stepped (no action / non-finite action): the stored state stands
+#pragma unroll
+                for (int e = 0; e < HUM_NSTATE; e++) st[e] = ((const T*)a.phys)[(long)e * a.n + i];
+            } else {
+                carry[0] = b.expect_high;
+                carry[1] = (int)(unsigned)(b.terrain_key & 0xffffffffull);
+                carry[2] = (int)(unsigned)(b.terrain_key >> 32);
+            }
+#pragma unroll
+            for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];
+        }
+        __syncthreads();
+    }
+    }   // steps of the launch
 #ifdef HUM_WLOG_ON
     if (threadIdx.x == 0) {   // wave duration: max (tail) and mean
         const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t_wave0;
@@ -782,7 +841,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         }
     }
 #endif
-    if (ef) atomicOr(a.eflags, ef);
+    if (ef) atomicOr(a0.eflags, ef);
 }
 
 template <typename T>

@@ -1,8 +1,8 @@
 // physics_group.h - cooperative (16 lanes per env) version of the humanoid substep.
 //
 // MI355X mapping: a 64-lane wavefront = 4 envs x 16 lanes; each env's working set lives in LDS
-// (struct GroupLDS, ~17.6 KB fp32), so a CU holds 8 envs (2 blocks) with no scratch spills and a
-// compact instruction stream.  Same algorithm and operation order as physics.h (the per-lane kernel,
+// (struct GroupLDS, ~10 KB fp32), so a CU holds 16 envs (4 blocks of one wave: one wave per SIMD, the CU's
+// 160 KB) with no scratch spills and a compact instruction stream.  Same algorithm and operation order as physics.h (the per-lane kernel,
 // kept as the reference-shaped variant) except for the order of floating-point sums inside the
 // element-parallel ABA backward pass and the 16-lane DPP reductions of the PGS row products.
 //

@@ -22,6 +22,7 @@
 #include "../../include/humanoid_env.h"
 
 void hum_internal_set_error(const char* msg);
+int hum_internal_device(const hum_env* env);   // humanoid_env.hip
 
 namespace {
 
@@ -37,7 +38,7 @@ struct PolicyArgs {
     const float* w1; const float* b1; const float* w2; const float* b2; const float* w3; const float* b3;
     const float* log_std;
     const float* obs; const float* obs_reset; const unsigned char* done;
-    float* act; float* mean_out; float* obs_in_out;
+    float* act; float* mean_out; float* obs_in_out; float* raw_out;
     int n, explore;
     unsigned long long seed, step;
 };
@@ -132,12 +133,14 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
                 const float mean = o[q] + p.b3[c3];
                 float a = mean;
                 if (p.explore) {   // DiagGaussian sample: mean + exp(log_std) * N(0, 1), counter-based Box-Muller
-                    const unsigned long long x = mix64(p.seed ^ mix64(((unsigned long long)i << 32) ^ (p.step * 32 + c3)));
+                    // (seed, lane, step, column) each through its own mixing round: no two triples share a draw
+                    const unsigned long long x = mix64(mix64(mix64(p.seed ^ (unsigned long long)i) ^ p.step) ^ (unsigned long long)c3);
                     const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;   // (0, 1]
                     const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
                     a = mean + expf(p.log_std[c3]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
                 }
                 p.act[(long)i * ACT + c3] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
+                if (p.raw_out) p.raw_out[(long)i * ACT + c3] = a;           // the sample itself (SampleBatch actions)
                 if (p.mean_out) p.mean_out[(long)i * ACT + c3] = mean;
             }
         }
@@ -213,6 +216,12 @@ int hum_policy_destroy(hum_policy* p) {
 
 int hum_policy_act(hum_policy* p, const float* obs, const float* obs_reset, const uint8_t* done, int32_t n,
                    float* actions, float* mean_out, float* obs_in_out, int32_t explore, uint64_t step, void* stream) {
+    return hum_policy_act_ex(p, obs, obs_reset, done, n, actions, mean_out, obs_in_out, nullptr, explore, step, stream);
+}
+
+int hum_policy_act_ex(hum_policy* p, const float* obs, const float* obs_reset, const uint8_t* done, int32_t n,
+                      float* actions, float* mean_out, float* obs_in_out, float* raw_out, int32_t explore, uint64_t step,
+                      void* stream) {
     if (!p || !obs || !actions || n <= 0) return perr(HUM_ERR_ARG, "hum_policy_act: bad argument");
     if ((obs_reset == nullptr) != (done == nullptr)) return perr(HUM_ERR_ARG, "hum_policy_act: obs_reset needs done");
     if (hipSetDevice(p->device) != hipSuccess) return perr(HUM_ERR_HIP, "hum_policy_act: hipSetDevice");
@@ -220,6 +229,7 @@ int hum_policy_act(hum_policy* p, const float* obs, const float* obs_reset, cons
     a.f1 = p->f1; a.f2 = p->f2; a.f3 = p->f3;
     a.w1 = p->w1; a.b1 = p->b1; a.w2 = p->w2; a.b2 = p->b2; a.w3 = p->w3; a.b3 = p->b3; a.log_std = p->log_std;
     a.obs = obs; a.obs_reset = obs_reset; a.done = done; a.act = actions; a.mean_out = mean_out; a.obs_in_out = obs_in_out;
+    a.raw_out = raw_out;
     a.n = n; a.explore = explore; a.seed = p->seed; a.step = step;
     hipLaunchKernelGGL(policy_kernel, dim3((n + ROWS - 1) / ROWS), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
     const hipError_t st = hipGetLastError();
@@ -229,27 +239,28 @@ int hum_policy_act(hum_policy* p, const float* obs, const float* obs_reset, cons
 
 // k sampler steps on the env's lanes with no host round trip: policy (on the current observation; lanes that
 // finished an episode in the previous step act on their reset observation) -> hum_step with auto-reset.
-// Trajectory outputs (device, any may be NULL): obs_traj [k,n,70] the policy's inputs, act_traj [k,n,17],
-// rew_traj [k,n], done_traj [k,n].  obs / obs_reset / done / reward are the env-step buffers (device [n,70],
-// [n,70], [n], [n]); on entry obs holds the current observation and done the previous step's flags (zeros after
-// a reset).  Launches go to `stream` in order.
+// Trajectory outputs (device, any may be NULL): obs_traj [k,n,70] the policy's inputs, act_traj [k,n,17] the
+// sampled actions before clip_actions (what RLlib's SampleBatch records and PPO's likelihood ratio is evaluated on;
+// the env receives their clip to [-1, 1]), rew_traj [k,n], done_traj [k,n].  obs / obs_reset / done / reward are the
+// env-step buffers (device [n,70], [n,70], [n], [n]); on entry obs holds the current observation and done the
+// previous step's flags (zeros after a reset).  Launches go to `stream` in order.
 int hum_rollout(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_t step0, float* obs, float* obs_reset,
                 uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj, float* rew_traj,
                 uint8_t* done_traj, void* stream) {
     if (!env || !p || k <= 0 || !obs || !obs_reset || !done || !reward || !act_buf)
         return perr(HUM_ERR_ARG, "hum_rollout: bad argument");
+    if (hum_internal_device(env) != p->device)
+        return perr(HUM_ERR_ARG, "hum_rollout: the env handle and the policy are on different devices");
     const int n = hum_num_lanes(env);
     hipStream_t s = (hipStream_t)stream;
     for (int t = 0; t < k; t++) {
-        int rc = hum_policy_act(p, obs, obs_reset, done, n, act_buf, nullptr,
-                                obs_traj ? obs_traj + (size_t)t * n * HUM_NOBS : nullptr, explore, step0 + (uint64_t)t,
-                                stream);
+        int rc = hum_policy_act_ex(p, obs, obs_reset, done, n, act_buf, nullptr,
+                                   obs_traj ? obs_traj + (size_t)t * n * HUM_NOBS : nullptr,
+                                   act_traj ? act_traj + (size_t)t * n * HUM_NACT : nullptr, explore,
+                                   step0 + (uint64_t)t, stream);
         if (rc != HUM_OK) return rc;
         rc = hum_step(env, act_buf, obs, reward, done, nullptr, HUM_STEP_AUTORESET, obs_reset, stream);
         if (rc != HUM_OK) return rc;
-        if (act_traj && hipMemcpyAsync(act_traj + (size_t)t * n * HUM_NACT, act_buf, (size_t)n * HUM_NACT * sizeof(float),
-                                       hipMemcpyDeviceToDevice, s) != hipSuccess)
-            return perr(HUM_ERR_HIP, "hum_rollout: act copy");
         if (rew_traj && hipMemcpyAsync(rew_traj + (size_t)t * n, reward, (size_t)n * sizeof(float),
                                        hipMemcpyDeviceToDevice, s) != hipSuccess)
             return perr(HUM_ERR_HIP, "hum_rollout: reward copy");

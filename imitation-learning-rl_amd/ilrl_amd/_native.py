@@ -8,11 +8,11 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", os.path.join(HERE, "_lib", "libhumenv.so"))
 
-HUM_ABI_VERSION = 7   # include/humanoid_env.h
+HUM_ABI_VERSION = 8   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
-HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS = 1, 2
+HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS, HUM_STEP_HOST_IO, HUM_STEP_CHECK_FINITE = 1, 2, 4, 8
 HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
 HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW, HUM_EFLAG_BAD_START_FRAME = 1, 2, 4, 8
 HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
@@ -40,7 +40,8 @@ EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_creat
            "hum_step_graph", "hum_get_aux", "hum_get_state", "hum_set_state", "hum_get_parts",
            "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step",
            "hum_reset_ex", "hum_hier_reset_ex", "hum_clip_csv_sizes", "hum_clip_csv_parse", "hum_load_clip_csv",
-           "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout", "hum_set_terrain"]
+           "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout", "hum_set_terrain",
+           "hum_step_k", "hum_hier_step_k", "hum_set_terrain_ex", "hum_policy_act_ex"]
 
 
 class HumConfig(ctypes.Structure):
@@ -86,6 +87,7 @@ def lib():
     L.hum_set_lane_modes.argtypes = [vp, vp]
     L.hum_set_predefined_targets.argtypes = [vp, dp, i32]
     L.hum_set_terrain.argtypes = [vp, i32, vp, i32, i32, dp, dp]
+    L.hum_set_terrain_ex.argtypes = [vp, i32, vp, i32, i32, dp, dp, dp]
     L.hum_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hum_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.hum_clip_csv_sizes.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i32)]
@@ -94,11 +96,14 @@ def lib():
     L.hum_policy_create.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(vp)]
     L.hum_policy_destroy.argtypes = [vp]
     L.hum_policy_act.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, u64, vp]
+    L.hum_policy_act_ex.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, i32, u64, vp]
     L.hum_rollout.argtypes = [vp, vp, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.hum_hier_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.hum_step.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, vp]
+    L.hum_step_k.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, i32, vp]
     L.hum_hier_reset.argtypes = [vp, vp, vp, vp, vp, vp]
     L.hum_hier_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp]
+    L.hum_hier_step_k.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, i32, vp]
     L.hum_step_graph.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, i32]
     L.hum_get_aux.argtypes = [vp, vp, vp]
     L.hum_get_state.argtypes = [vp, dp, dp]

@@ -50,6 +50,7 @@ class HierVecEnv(HumanoidVecEnv):
         m, sf, ry, flags = self._reset_args(mask, start_frame, reset_yaw, start_from_ref, init_vel)
         N.check(N.lib().hum_hier_reset_ex(self.h, _ptr(m), _ptr(sf), _ptr(ry), flags, _ptr(self.obs_high),
                                           self._stream()), "hum_hier_reset")
+        self._clear_done(m)
         return self.obs_high
 
     def _act(self, a, width, zero):
@@ -73,6 +74,30 @@ class HierVecEnv(HumanoidVecEnv):
                                       _ptr(self.frame), flags, _ptr(self.obs_high_reset), self._stream()),
                 "hum_hier_step")
         return self.agents, self.obs_high, self.obs, self.reward_high, self.reward, self.done, self.frame
+
+    def step_k(self, high_actions, low_actions, agent=None, autoreset=False, skip_physics=False, out=None):
+        """k agent transitions per lane in one launch (hum_hier_step_k).  high_actions [k,n,2], low_actions
+        [k,n,17], agent [k,n] u8 or None (each lane's expected agent).  Returns device tensors (agents [k,n],
+        obs_high [k,n,44], obs_low [k,n,70], rew_high [k,n], rew_low [k,n], done [k,n], frame [k,n],
+        obs_high_reset [k,n,44]): row t is the t-th of k step() calls."""
+        t = self.torch
+        ah = t.as_tensor(high_actions, dtype=t.float32, device=self.device).contiguous()
+        al = t.as_tensor(low_actions, dtype=t.float32, device=self.device).contiguous()
+        k = ah.shape[0]
+        if ah.shape != (k, self.n, N.HUM_NACT_HIGH) or al.shape != (k, self.n, N.HUM_NACT):
+            raise ValueError("actions must be [k, %d, 2] and [k, %d, 17]" % (self.n, self.n))
+        ag = None if agent is None else t.as_tensor(agent, dtype=t.uint8, device=self.device).expand(k, self.n).contiguous()
+        if out is None or out[0].shape[0] != k:
+            f32 = t.float32
+            z = lambda *s, d=f32: t.zeros(*s, dtype=d, device=self.device)
+            out = (z(k, self.n, d=t.uint8), z(k, self.n, N.HUM_NOBS_HIGH), z(k, self.n, N.HUM_NOBS), z(k, self.n),
+                   z(k, self.n), z(k, self.n, d=t.uint8), z(k, self.n, d=t.int32), z(k, self.n, N.HUM_NOBS_HIGH))
+        agents, oh, ol, rh, rl, done, frame, ohr = out
+        flags = (N.HUM_STEP_AUTORESET if autoreset else 0) | (N.HUM_STEP_SKIP_PHYSICS if skip_physics else 0)
+        N.check(N.lib().hum_hier_step_k(self.h, _ptr(ah), _ptr(al), _ptr(ag), _ptr(agents), _ptr(oh), _ptr(ol),
+                                        _ptr(rh), _ptr(rl), _ptr(done), _ptr(frame), flags, _ptr(ohr), k,
+                                        self._stream()), "hum_hier_step_k")
+        return out
 
 
 class _HierBookView(_BookView):

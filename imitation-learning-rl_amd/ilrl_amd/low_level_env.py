@@ -114,6 +114,7 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
         self.skipFrame = 2
         self.targetLen = 5
         self.max_frame = self._v.clips[0].max_frame
+        self.__dict__["_n_vel"] = int(self._v.clips[0].vel.shape[0])
         self.useCustomEnv = bool(useCustomEnv)
         if self.useCustomEnv:   # :41-42 CustomHumanoid: CustomScene's random heightfield instead of the plane
             self._v.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
@@ -157,25 +158,39 @@ class LowLevelHumanoidEnv(_BookView, _optional_base("gym", "Env")):
         if self.useCustomEnv and self._v.terrain != N.HUM_TERRAIN_RANDOM_BLOCKS:
             self._v.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
 
+    def _vel_row_check(self, when):
+        """The reference reads JointSpeedRadSec.iloc[frame] (low_level_env.py:208, :310, :345): motion13_13 has 120
+        velocity rows for 220 pose rows, so once the frame reaches the table's end pandas raises IndexError there.
+        (Vector / benchmark handles keep stepping on the clamped last row and flag HUM_EFLAG_VEL_ROW instead.)"""
+        if self.frame >= self._n_vel:
+            raise IndexError("single positional indexer is out-of-bounds (%s: frame %d, %d velocity rows)"
+                             % (when, self.frame, self._n_vel))
+
     def reset(self, resetYaw=0):                                        # low_level_env.py:224-232
         self._scene_restart()
-        return self._obs(self._v.reset(reset_yaw=float(resetYaw)))
+        o = self._obs(self._v.reset(reset_yaw=float(resetYaw)))
+        self._vel_row_check("reset")
+        return o
 
     def resetFromFrame(self, startFrame=0, resetYaw=0, startFromRef=True, initVel=True):   # :247-305
         if startFromRef and not 0 <= int(startFrame) < self.max_frame + 1:   # DataFrame.iloc (:208) raises
             raise IndexError("single positional indexer is out-of-bounds (startFrame=%d)" % int(startFrame))
         self._scene_restart()
-        return self._obs(self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw),
-                                       start_from_ref=startFromRef, init_vel=initVel))
+        o = self._obs(self._v.reset(start_frame=int(startFrame), reset_yaw=float(resetYaw),
+                                    start_from_ref=startFromRef, init_vel=initVel))
+        self._vel_row_check("resetFromFrame")
+        return o
 
     def step(self, action, debug=False):                                # :322-323, :475-526
         a = np.asarray(action, dtype=np.float32).reshape(1, 17)
         assert np.isfinite(a).all()                                     # humanoid.py:55
+        self._vel_row_check("step")                                     # :345 calcJointVelScore
         if bool(debug) != self._debug:
             self.__dict__["_debug"] = bool(debug)
             self._sync_modes()
         obs, rew, done, _ = self._v.step(a)
         o = self._obs(obs)
+        self._vel_row_check("step")                                     # :310 getLowLevelObs after incFrame
         return o, float(rew[0].item()), bool(done[0].item()), {}
 
     def close(self):
@@ -196,11 +211,15 @@ class _CustomSceneView:
         self._venv = venv
         self.heightfieldData = [0] * (self.numHeightfieldRows * self.numHeightfieldColumns)
 
+    # btHeightfieldTerrainShape's vertical centre from the CustomScene creation terrain (random blocks in [0, 0.5)
+    # with a zero centre patch: (min + max) / 2 ~ 0.25); pybullet's replaceHeightfieldIndex path keeps it
+    CREATION_CENTRE = 0.25
+
     def replaceHeightfieldData(self, newData):
         self.heightfieldData = list(newData)
         self._venv.set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=np.asarray(self.heightfieldData, dtype=np.float32),
                                w=self.numHeightfieldRows, l=self.numHeightfieldColumns, scale=(1.0, 1.0, 1.0),
-                               origin=(0.0, 0.0, 0.25))
+                               origin=(0.0, 0.0, 0.25), centre=self.CREATION_CENTRE)
 
 
 class _CustomEnvView:
@@ -297,10 +316,10 @@ class HumanoidVectorEnv(_optional_base("ray.rllib.env.vector_env", "VectorEnv"))
 
     def vector_step(self, actions):
         a = np.asarray(actions, dtype=np.float32).reshape(self.num_envs, 17)
+        if not np.isfinite(a).all():   # humanoid.py:55, checked on the host copy RLlib hands over (no device sync)
+            raise AssertionError("non-finite action (humanoid.py:55)")
         obs, rew, done, _ = self.venv.step(a, autoreset=True)
         o, r, d = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy().astype(bool)
-        if self.venv.error_flags() & N.HUM_EFLAG_NONFINITE_ACTION:
-            raise AssertionError("non-finite action (humanoid.py:55)")
         self._reset_obs = self.venv.obs_reset.cpu().numpy()
         self._reset_pending = d.copy()
         self._invalidate()

@@ -87,20 +87,23 @@ class DevicePolicy:
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def act(self, obs, obs_reset=None, done=None, explore=False, step=0, out=None, mean_out=None):
-        """actions [n,17] (device) for device observations obs [n,70] (done lanes read obs_reset)."""
+    def act(self, obs, obs_reset=None, done=None, explore=False, step=0, out=None, mean_out=None, raw_out=None):
+        """actions [n,17] (device, clipped to the Box) for device observations obs [n,70] (done lanes read
+        obs_reset); raw_out receives the samples before clip_actions (RLlib's SampleBatch actions)."""
         t = self.torch
         n = obs.shape[0]
         act = out if out is not None else t.empty(n, N.HUM_NACT, dtype=t.float32, device=self.device)
         p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
-        N.check(N.lib().hum_policy_act(self.h, p(obs), p(obs_reset), p(done), n, p(act), p(mean_out), None,
-                                       int(bool(explore)), ctypes.c_uint64(step), self._stream()), "hum_policy_act")
+        N.check(N.lib().hum_policy_act_ex(self.h, p(obs), p(obs_reset), p(done), n, p(act), p(mean_out), None,
+                                          p(raw_out), int(bool(explore)), ctypes.c_uint64(step), self._stream()),
+                "hum_policy_act")
         return act
 
     def rollout(self, venv, k, explore=True, step0=0, trajectories=True):
         """k sampler steps (policy -> env step with auto-reset) on venv's lanes, all on the device with no host
         round trip.  venv.obs must hold the current observation (after venv.reset()).  Returns the trajectory
-        tensors {obs [k,n,70] (policy inputs), actions [k,n,17], rewards [k,n], dones [k,n]} (or {})."""
+        tensors {obs [k,n,70] (policy inputs), actions [k,n,17] (the samples before clip_actions, as RLlib records
+        them), rewards [k,n], dones [k,n]} (or {})."""
         t = self.torch
         n = venv.n
         if not hasattr(venv, "_act_buf"):

@@ -80,9 +80,11 @@ class HumanoidVecEnv:
             m |= np.where(np.broadcast_to(predefined, self.n), N.HUM_MODE_PREDEFINED, 0).astype(np.uint32)
         N.check(N.lib().hum_set_lane_modes(self.h, m.ctypes.data_as(ctypes.c_void_p)), "hum_set_lane_modes")
 
-    def set_terrain(self, mode, heights=None, w=256, l=256, scale=(1.0, 1.0, 1.0), origin=(0.0, 0.0, 0.25)):
-        """Ground of every lane (hum_set_terrain): N.HUM_TERRAIN_PLANE, N.HUM_TERRAIN_HEIGHTFIELD (heights [w*l],
-        vertex (i, j) = heights[i + j*w], CustomScene.replaceHeightfieldData's layout) or
+    def set_terrain(self, mode, heights=None, w=256, l=256, scale=(1.0, 1.0, 1.0), origin=(0.0, 0.0, 0.25),
+                    centre=None):
+        """Ground of every lane (hum_set_terrain_ex): N.HUM_TERRAIN_PLANE, N.HUM_TERRAIN_HEIGHTFIELD (heights [w*l],
+        vertex (i, j) = heights[i + j*w], CustomScene.replaceHeightfieldData's layout; centre = the vertical centre
+        Bullet keeps from the shape's creation, None = (min + max) / 2 of these heights) or
         N.HUM_TERRAIN_RANDOM_BLOCKS (LowLevelHumanoidEnv(useCustomEnv=True): a new CustomScene terrain per lane at
         every reset)."""
         h = None
@@ -92,8 +94,9 @@ class HumanoidVecEnv:
                 raise ValueError("heights: %d values for a %d x %d heightfield" % (h.size, w, l))
         sc = np.ascontiguousarray(scale, dtype=np.float64)
         org = np.ascontiguousarray(origin, dtype=np.float64)
-        N.check(N.lib().hum_set_terrain(self.h, int(mode), h.ctypes.data if h is not None else None, int(w), int(l),
-                                        _dp(sc), _dp(org)), "hum_set_terrain")
+        ctr = None if centre is None else np.array([float(centre)], dtype=np.float64)
+        N.check(N.lib().hum_set_terrain_ex(self.h, int(mode), h.ctypes.data if h is not None else None, int(w), int(l),
+                                           _dp(sc), _dp(org), _dp(ctr) if ctr is not None else None), "hum_set_terrain")
         self.terrain = int(mode)
 
     def set_predefined_targets(self, xyz):
@@ -110,11 +113,19 @@ class HumanoidVecEnv:
 
     def reset(self, mask=None, start_frame=None, reset_yaw=None, start_from_ref=True, init_vel=True):
         """reset()/resetFromFrame(startFrame, resetYaw, startFromRef, initVel) for masked lanes; returns the obs
-        tensor [n,70] (device)."""
+        tensor [n,70] (device).  The reset lanes' done flags are cleared: `done` then means "the last step ended
+        the episode" for the policy / rollout loops that read it (hum_rollout, DevicePolicy.act)."""
         m, sf, ry, flags = self._reset_args(mask, start_frame, reset_yaw, start_from_ref, init_vel)
         N.check(N.lib().hum_reset_ex(self.h, _ptr(m), _ptr(sf), _ptr(ry), flags, _ptr(self.obs), self._stream()),
                 "hum_reset")
+        self._clear_done(m)
         return self.obs
+
+    def _clear_done(self, m):
+        if m is None:
+            self.done.zero_()
+        else:
+            self.done.masked_fill_(m.bool(), 0)
 
     def step(self, actions, autoreset=False, skip_physics=False):
         """One env step for all lanes. actions: float32 [n,17] (device tensor or array)."""
@@ -126,6 +137,28 @@ class HumanoidVecEnv:
         N.check(N.lib().hum_step(self.h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
                                  _ptr(self.frame), flags, _ptr(self.obs_reset), self._stream()), "hum_step")
         return self.obs, self.reward, self.done, self.frame
+
+    def step_k(self, actions, autoreset=False, skip_physics=False, out=None):
+        """k env steps for all lanes in one launch (hum_step_k).  actions: float32 [k,n,17]; returns device tensors
+        (obs [k,n,70], reward [k,n], done [k,n], frame [k,n], obs_reset [k,n,70]) - row t is what the t-th of k
+        step() calls returns.  `out` reuses a previous call's tuple of the same k."""
+        t = self.torch
+        a = t.as_tensor(actions, dtype=t.float32, device=self.device).contiguous()
+        if a.dim() != 3 or a.shape[1:] != (self.n, N.HUM_NACT):
+            raise ValueError("actions must be [k, %d, %d], got %s" % (self.n, N.HUM_NACT, tuple(a.shape)))
+        k = a.shape[0]
+        if out is None or out[0].shape[0] != k:
+            f32 = t.float32
+            out = (t.zeros(k, self.n, N.HUM_NOBS, dtype=f32, device=self.device),
+                   t.zeros(k, self.n, dtype=f32, device=self.device),
+                   t.zeros(k, self.n, dtype=t.uint8, device=self.device),
+                   t.zeros(k, self.n, dtype=t.int32, device=self.device),
+                   t.zeros(k, self.n, N.HUM_NOBS, dtype=f32, device=self.device))
+        obs, rew, done, frame, obs_reset = out
+        flags = (N.HUM_STEP_AUTORESET if autoreset else 0) | (N.HUM_STEP_SKIP_PHYSICS if skip_physics else 0)
+        N.check(N.lib().hum_step_k(self.h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done), _ptr(frame), flags,
+                                   _ptr(obs_reset), k, self._stream()), "hum_step_k")
+        return out
 
     def get_aux(self):
         N.check(N.lib().hum_get_aux(self.h, _ptr(self.aux), self._stream()), "hum_get_aux")

@@ -12,7 +12,8 @@
  *   - extern "C", plain pointers + sizes, int status (0 = ok, < 0 = error, hum_last_error() for text);
  *     no exceptions cross the ABI.
  *   - Hot-path I/O (actions, obs, reward, done, frame) are DEVICE pointers on the handle's GPU (e.g.
- *     torch.cuda tensors) - zero-copy.  State get/set use HOST pointers (bulk copies for parity tests).
+ *     torch.cuda tensors) - zero-copy - or, with HUM_STEP_HOST_IO, host pointers (staged through the device and
+ *     synchronised before the call returns).  State get/set use HOST pointers (bulk copies for parity tests).
  *   - `stream` is a hipStream_t (NULL = the HIP null stream; hum_stream() returns the handle's own
  *     stream).  Launches are asynchronous on that stream; state get/set, error flags and hum_sync
  *     synchronise the device.  A handle is bound to one device and is not thread-safe.
@@ -34,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 7
+#define HUM_ABI_VERSION 8
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -55,6 +56,12 @@ extern "C" {
 /* hum_step flags */
 #define HUM_STEP_AUTORESET 1u     /* reset done lanes inside the same launch (obs_reset receives the new obs) */
 #define HUM_STEP_SKIP_PHYSICS 2u  /* treat the current physics state as post-step (parity: injected physics) */
+#define HUM_STEP_HOST_IO 4u       /* actions / outputs are HOST pointers: copied to and from the device around the
+                                     launch on `stream`, which the call then synchronises (the gym view's path) */
+#define HUM_STEP_CHECK_FINITE 8u  /* wait for the launch and return HUM_ERR_ARG if a lane's action was non-finite
+                                     (humanoid.py:55 `assert np.isfinite(a).all()`; those lanes are not stepped and
+                                     the sticky HUM_EFLAG_NONFINITE_ACTION bit is consumed).  Without it the launch
+                                     stays asynchronous and only the sticky bit records the event. */
 
 /* hum_reset_ex / hum_hier_reset_ex flags: resetFromFrame(startFromRef, initVel) (low_level_env.py:247-305,
  * hier_env.py:259-319); both False-able independently, default (0) = True, True as reset() uses */
@@ -200,7 +207,7 @@ int hum_load_clip_csv(hum_env* env, int32_t clip_id, const char* dir, const char
  *     order: i along x), mesh scale scale3, body at origin3 (identity orientation); Bullet's btHeightfieldTerrainShape
  *     geometry: vertex (i, j) at origin + scale * (i - (w-1)/2, j - (l-1)/2, h - (min + max)/2), two triangles per
  *     cell split by diamond subdivision.  CustomScene.replaceHeightfieldData(d) = (d, 256, 256, {1,1,1}, {0,0,0.25}).
- *     Requires scale x, y >= 0.25 (a contact candidate reaches at most 2 x 2 cells).
+ *     Requires scale x, y >= 0.25 (a candidate then tests at most 2 x 2 cells per substep).
  *   HUM_TERRAIN_RANDOM_BLOCKS: CustomScene.episode_restart's terrain per lane, regenerated at every reset: 256 x 256
  *     vertices in 2 x 2 blocks of height random.uniform(0, 0.05) * 10, the four centre blocks 0, body at
  *     (0, 0, 0.25); block heights are counter-based draws from the lane's terrain key (HUM_BK_TERRAIN_KEY_*),
@@ -210,6 +217,12 @@ int hum_load_clip_csv(hum_env* env, int32_t clip_id, const char* dir, const char
  * cells within reach).  A captured step graph is recaptured. */
 int hum_set_terrain(hum_env* env, int32_t mode, const float* heights, int32_t w, int32_t l, const double* scale3,
                     const double* origin3);
+/* hum_set_terrain with the heightfield's vertical centre given: Bullet's btHeightfieldTerrainShape centres the data
+ * on (min + max) / 2 of the heights it was CREATED with, and pybullet's createCollisionShape(replaceHeightfieldIndex=
+ * ...) - CustomScene.replaceHeightfieldData, humanoid.py:75-85 - replaces the heights but keeps that centre (the
+ * CustomScene creation terrain's, 0.25).  centre NULL = (min + max) / 2 of `heights` (a newly created shape). */
+int hum_set_terrain_ex(hum_env* env, int32_t mode, const float* heights, int32_t w, int32_t l, const double* scale3,
+                       const double* origin3, const double* centre);
 
 /* clip id per lane (host array of n_lanes); default all 0 */
 int hum_set_lane_clips(hum_env* env, const int32_t* clip_of_lane);
@@ -235,6 +248,16 @@ int hum_reset_ex(hum_env* env, const uint8_t* lane_mask, const int32_t* start_fr
  * written to obs_reset (device [n,70], may be NULL) while `obs` keeps the terminal observation. */
 int hum_step(hum_env* env, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
              uint32_t flags, float* obs_reset, void* stream);
+
+/* k env steps for all lanes in ONE launch (the loop RLlib's sampler runs over a rollout fragment,
+ * low_level_env.py:475-526 per step): actions [k,n,17] f32 -> obs [k,n,70], reward [k,n], done [k,n],
+ * frame [k,n] (may be NULL); step t reads actions[t] and writes row t of every output, and with
+ * HUM_STEP_AUTORESET a lane done at step t is reset before step t + 1 (obs_reset [k,n,70], rows of the lanes
+ * reset at step t written, may be NULL).  Results are identical to k hum_step calls on the same buffers' rows;
+ * each env's working set stays on chip between its steps, and a fast wavefront runs ahead instead of waiting
+ * for the slowest one of every launch.  k = 1 is hum_step. */
+int hum_step_k(hum_env* env, const float* actions, float* obs, float* reward, uint8_t* done, int32_t* frame,
+               uint32_t flags, float* obs_reset, int32_t k, void* stream);
 
 /* Capture `k` consecutive steps (same buffers, same flags) in a hipGraph and replay it on the handle's
  * own stream (hum_stream()); inputs must be ready (synchronise the producing stream first). */
@@ -262,6 +285,14 @@ int hum_hier_step(hum_env* env, const float* high_act, const float* low_act, con
                   float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
                   uint32_t flags, float* high_obs_reset, void* stream);
 
+/* k agent transitions per lane in ONE launch (hum_hier_step's semantics per transition): every per-transition
+ * array gains a leading [k] axis (high_act [k,n,2], low_act [k,n,17], agent [k,n] or NULL, agents [k,n],
+ * high_obs [k,n,44], low_obs [k,n,70], high_rew / low_rew / done / frame [k,n], high_obs_reset [k,n,44]).
+ * With agent == NULL every lane applies the action of the agent it expects at that transition. */
+int hum_hier_step_k(hum_env* env, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
+                    float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
+                    uint32_t flags, float* high_obs_reset, int32_t k, void* stream);
+
 /* ---- On-GPU policy inference: the reference's PPO policy network (train_config.py:107-111,
  * RLlib FullyConnectedNetwork, fcnet_hiddens [256, 256], tanh, free_log_std) evaluated on the env's device
  * buffers, so a sampler loop needs no host round trip.  Weights: host float32, TF kernel layout [in][out]:
@@ -276,10 +307,17 @@ int hum_policy_destroy(hum_policy* policy);
  * counter-based: (seed, lane, step, action index). */
 int hum_policy_act(hum_policy* policy, const float* obs, const float* obs_reset, const uint8_t* done, int32_t n,
                    float* actions, float* mean_out, float* obs_in_out, int32_t explore, uint64_t step, void* stream);
+/* hum_policy_act that also returns raw_out [n,17] (device, may be NULL): the sample before clip_actions, i.e. the
+ * action RLlib's SampleBatch records and PPO evaluates its likelihood ratio on. */
+int hum_policy_act_ex(hum_policy* policy, const float* obs, const float* obs_reset, const uint8_t* done, int32_t n,
+                      float* actions, float* mean_out, float* obs_in_out, float* raw_out, int32_t explore, uint64_t step,
+                      void* stream);
 /* k sampler steps (policy -> hum_step with HUM_STEP_AUTORESET) on `stream` with no host round trip.  obs,
  * obs_reset, done, reward: the env-step buffers (device [n,70], [n,70], [n], [n]); on entry obs holds the current
  * observation and done the previous step's flags (zeros after a reset); act_buf [n,17] scratch.  Optional device
- * trajectory outputs: obs_traj [k,n,70] (the policy inputs), act_traj [k,n,17], rew_traj [k,n], done_traj [k,n]. */
+ * trajectory outputs: obs_traj [k,n,70] (the policy inputs), act_traj [k,n,17] (the samples before clip_actions, as
+ * RLlib records them; the env steps on their clip), rew_traj [k,n], done_traj [k,n].  The env handle and the policy
+ * must be on the same device (HUM_ERR_ARG otherwise). */
 int hum_rollout(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
                 float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
                 float* rew_traj, uint8_t* done_traj, void* stream);

@@ -80,7 +80,7 @@ class Terrain:
     at heights[i + j*w]), mesh scale and body origin as CustomScene / pybullet take them; TERRAIN_RANDOM_BLOCKS =
     CustomScene.episode_restart's terrain (humanoid.py:89-113) regenerated at every reset from a per-env key."""
 
-    def __init__(self, mode, heights=None, w=256, l=256, scale=(1.0, 1.0, 1.0), origin=(0.0, 0.0, 0.25)):
+    def __init__(self, mode, heights=None, w=256, l=256, scale=(1.0, 1.0, 1.0), origin=(0.0, 0.0, 0.25), centre=None):
         self.mode = mode
         self.w, self.l = w, l
         self.scale, self.origin = tuple(scale), tuple(origin)
@@ -89,7 +89,9 @@ class Terrain:
         if mode == TERRAIN_HEIGHTFIELD:
             self.heights = np.ascontiguousarray(heights, dtype=np.float32).reshape(-1)
             assert self.heights.size == w * l
-            self.mid = 0.5 * (float(self.heights.min()) + float(self.heights.max()))   # btHeightfieldTerrainShape
+            # btHeightfieldTerrainShape: (min + max) / 2 of the creation data; a replaceHeightfieldIndex update keeps
+            # the creation value (hum_set_terrain_ex's centre)
+            self.mid = 0.5 * (float(self.heights.min()) + float(self.heights.max())) if centre is None else float(centre)
 
     def apply(self, P, key=0):
         P.terrain = self.mode

@@ -111,3 +111,134 @@ def test_load_clip_csv_on_device_equals_packed_clip():
     assert b"cannot open" in N.lib().hum_last_error()
     for e in envs:
         e.close()
+
+
+def _p(x):
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        return N.ctypes.c_void_p(x.ctypes.data)
+    return N.ctypes.c_void_p(x.data_ptr())
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_host_io_equals_device_path(k):
+    """HUM_STEP_HOST_IO (buffers may be host or device pointers, flag): host numpy buffers give the
+    device path's results bit for bit, and rows the step leaves unwritten (obs_reset of lanes not done) keep the
+    caller's values."""
+    n = 64
+    envs = [HumanoidVecEnv(n, clips=("motion02_04",), seed=21) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    rng = np.random.default_rng(2)
+    for it in range(6):
+        a = rng.uniform(-1, 1, (k, n, 17)).astype(np.float32)
+        dev = envs[0].step_k(torch.as_tensor(a, device="cuda"), autoreset=True)
+        obs = np.zeros((k, n, 70), np.float32)
+        rew = np.zeros((k, n), np.float32)
+        done = np.zeros((k, n), np.uint8)
+        frame = np.zeros((k, n), np.int32)
+        orst = np.full((k, n, 70), 7.0, np.float32)
+        rc = N.lib().hum_step_k(envs[1].h, _p(a), _p(obs), _p(rew), _p(done), _p(frame),
+                                N.HUM_STEP_AUTORESET | N.HUM_STEP_HOST_IO, _p(orst), k, None)
+        assert rc == 0, N.lib().hum_last_error()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(obs, dev[0].cpu().numpy())
+        np.testing.assert_array_equal(rew, dev[1].cpu().numpy())
+        np.testing.assert_array_equal(done, dev[2].cpu().numpy())
+        np.testing.assert_array_equal(frame, dev[3].cpu().numpy())
+        dm = done.astype(bool)
+        np.testing.assert_array_equal(orst[dm], dev[4].cpu().numpy()[dm])
+        assert (orst[~dm] == 7.0).all()
+    p0, b0 = envs[0].get_state()
+    p1, b1 = envs[1].get_state()
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(b0, b1)
+    for e in envs:
+        e.close()
+
+
+def test_hier_host_io_equals_device_path():
+    n = 32
+    envs = [HierVecEnv(n, seed=3) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    rng = np.random.default_rng(4)
+    for it in range(12):
+        ah = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        al = rng.uniform(-1, 1, (n, 17)).astype(np.float32)
+        dev = [x.cpu().numpy() for x in envs[0].step(ah, al, autoreset=True)]
+        agents = np.zeros(n, np.uint8)
+        oh = np.zeros((n, 44), np.float32)
+        ol = np.zeros((n, 70), np.float32)
+        rh = np.zeros(n, np.float32)
+        rl = np.zeros(n, np.float32)
+        done = np.zeros(n, np.uint8)
+        frame = np.zeros(n, np.int32)
+        rc = N.lib().hum_hier_step(envs[1].h, _p(ah), _p(al), None, _p(agents), _p(oh), _p(ol), _p(rh), _p(rl),
+                                   _p(done), _p(frame), N.HUM_STEP_AUTORESET | N.HUM_STEP_HOST_IO, None, None)
+        assert rc == 0, N.lib().hum_last_error()
+        np.testing.assert_array_equal(agents, dev[0])
+        hi, lo = (agents & N.HUM_AGENT_HIGH) != 0, (agents & N.HUM_AGENT_LOW) != 0
+        np.testing.assert_array_equal(oh[hi], dev[1][hi])
+        np.testing.assert_array_equal(ol[lo], dev[2][lo])
+        np.testing.assert_array_equal(rh, dev[3])
+        np.testing.assert_array_equal(rl, dev[4])
+        np.testing.assert_array_equal(done, dev[5])
+    p0, b0 = envs[0].get_state()
+    p1, b1 = envs[1].get_state()
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(b0, b1)
+    for e in envs:
+        e.close()
+
+
+def test_check_finite_returns_error_status():
+    """HUM_STEP_CHECK_FINITE: a non-finite action is an error status of the call itself (humanoid.py:55 assert);
+    the lane is not stepped, the others are, and the sticky bit is consumed."""
+    n = 16
+    env = HumanoidVecEnv(n, clips=("motion02_04",), seed=5)
+    env.reset()
+    p0, b0 = env.get_state()
+    a = np.random.default_rng(0).uniform(-1, 1, (n, 17)).astype(np.float32)
+    a[3, 4] = np.nan
+    obs = np.zeros((n, 70), np.float32)
+    rew = np.zeros(n, np.float32)
+    done = np.zeros(n, np.uint8)
+    rc = N.lib().hum_step(env.h, _p(a), _p(obs), _p(rew), _p(done), None,
+                          N.HUM_STEP_HOST_IO | N.HUM_STEP_CHECK_FINITE, None, None)
+    assert rc == N.HUM_ERR_ARG
+    assert b"non-finite action" in N.lib().hum_last_error()
+    p1, b1 = env.get_state()
+    np.testing.assert_array_equal(p1[3], p0[3])
+    np.testing.assert_array_equal(b1[3], b0[3])
+    assert (np.abs(p1[np.arange(n) != 3] - p0[np.arange(n) != 3]).max(axis=1) > 0).all()
+    assert env.error_flags() & N.HUM_EFLAG_NONFINITE_ACTION == 0
+    a[3, 4] = 0.5
+    rc = N.lib().hum_step(env.h, _p(a), _p(obs), _p(rew), _p(done), None,
+                          N.HUM_STEP_HOST_IO | N.HUM_STEP_CHECK_FINITE, None, None)
+    assert rc == N.HUM_OK
+    g = torch.zeros(n, 17, device="cuda")
+    assert N.lib().hum_step_graph(env.h, _p(g), _p(env.obs), _p(env.reward), _p(env.done), None,
+                                  N.HUM_STEP_CHECK_FINITE, None, 2) == N.HUM_ERR_ARG
+    env.close()
+
+
+def test_gym_view_raises_past_the_velocity_table():
+    """motion13_13 has 120 velocity rows for 220 pose rows: the reference's JointSpeedRadSec.iloc[frame] raises
+    IndexError once the frame reaches 120 (low_level_env.py:208, :310, :345); the single-env view raises likewise
+    (vector / bench handles keep the clamped row and flag HUM_EFLAG_VEL_ROW)."""
+    from ilrl_amd.low_level_env import LowLevelHumanoidEnv
+    env = LowLevelHumanoidEnv(reference_name="motion13_13", seed=1)
+    env.resetFromFrame(startFrame=115)          # frame 117
+    env.step(np.zeros(17, np.float32))          # frame 119
+    with pytest.raises(IndexError):
+        env.step(np.zeros(17, np.float32))      # getLowLevelObs at frame 121
+    with pytest.raises(IndexError):
+        env.step(np.zeros(17, np.float32))      # calcJointVelScore at frame 121
+    with pytest.raises(IndexError):
+        env.resetFromFrame(startFrame=118)      # obs row 120
+    env.resetFromFrame(startFrame=10)
+    o, r, d, _ = env.step(np.zeros(17, np.float32))
+    assert np.isfinite(o).all()
+    env.close()

@@ -54,21 +54,26 @@ def test_policy_done_lanes_read_reset_obs_and_exploration_noise():
 
 
 def test_rollout_equals_python_loop():
-    """hum_rollout (policy -> step with auto-reset, k launches pairs on one stream) == the same loop from Python."""
+    """hum_rollout (policy -> step with auto-reset, k launches pairs on one stream) == the same loop from Python.
+    The recorded actions are the samples before clip_actions (what RLlib's SampleBatch keeps for PPO's likelihood
+    ratio); the env steps on their clip.  reset() clears `done`: no manual zeroing before the rollout,
+    even after a previous episode left done lanes."""
     n, k = 512, 24
     pol = DevicePolicy.random_init(seed=9)
     envs = [HumanoidVecEnv(n, clips=("motion02_04",), seed=2) for _ in range(2)]
     for e in envs:
+        e.done.fill_(1)   # stale flags from an earlier episode
         e.reset()
-        e.done.zero_()
     tr = pol.rollout(envs[0], k, explore=True, step0=100)
     e = envs[1]
     act = torch.empty(n, 17, device="cuda")
+    raw = torch.empty(n, 17, device="cuda")
     for t in range(k):
         inp = torch.where(e.done.bool()[:, None], e.obs_reset, e.obs).clone()
         torch.testing.assert_close(tr["obs"][t], inp, atol=0, rtol=0)
-        pol.act(e.obs, e.obs_reset, e.done, explore=True, step=100 + t, out=act)
-        torch.testing.assert_close(tr["actions"][t], act, atol=0, rtol=0)
+        pol.act(e.obs, e.obs_reset, e.done, explore=True, step=100 + t, out=act, raw_out=raw)
+        torch.testing.assert_close(tr["actions"][t], raw, atol=0, rtol=0)
+        torch.testing.assert_close(tr["actions"][t].clamp(-1, 1), act, atol=0, rtol=0)
         e.step(act, autoreset=True)
         torch.testing.assert_close(tr["rewards"][t], e.reward, atol=0, rtol=0)
         assert torch.equal(tr["dones"][t], e.done)
@@ -77,6 +82,7 @@ def test_rollout_equals_python_loop():
     np.testing.assert_array_equal(p0, p1)
     np.testing.assert_array_equal(b0, b1)
     assert tr["dones"].sum().item() > 0
+    assert (tr["actions"].abs() > 1).any()   # samples past the Box bound are recorded unclipped
     for x in envs:
         x.close()
     pol.close()

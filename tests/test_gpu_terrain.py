@@ -141,14 +141,16 @@ def test_random_block_terrain_matches_oracle(precision):
     env.close()
 
 
-@pytest.mark.parametrize("precision", ["fp64", "fp32"])
-def test_ramp_heightfield_matches_oracle(precision):
+@pytest.mark.parametrize("precision,centre", [("fp64", None), ("fp32", None), ("fp64", 0.25), ("fp32", 0.25)])
+def test_ramp_heightfield_matches_oracle(precision, centre):
+    """centre None: a heightfield shape created from the ramp ((min + max) / 2 = 0.2); 0.25: the ramp installed by
+    CustomScene.replaceHeightfieldData, which keeps the creation terrain's centre (humanoid.py:75-85)."""
     n = 64
     clip = load_clip(CLIP)
     h = ramp_heights()
-    terrain = O.Terrain(O.TERRAIN_HEIGHTFIELD, heights=h, w=256, l=256, origin=(0.0, 0.0, 0.25))
+    terrain = O.Terrain(O.TERRAIN_HEIGHTFIELD, heights=h, w=256, l=256, origin=(0.0, 0.0, 0.25), centre=centre)
     env = HumanoidVecEnv(n, clips=(CLIP,), seed=5, precision=precision)
-    env.set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=h, w=256, l=256, origin=(0.0, 0.0, 0.25))
+    env.set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=h, w=256, l=256, origin=(0.0, 0.0, 0.25), centre=centre)
     env.reset()
     rng = np.random.default_rng(11)
     _place(env, terrain, rng, (-2.0, 9.0, -4.0, 4.0))
