@@ -66,30 +66,9 @@ struct KArgs {
     float* rew_high;                // [n]
     float* obs_high_reset;          // [n,44]
     // multi-step launch (hum_step_k / hum_hier_step_k): env steps per launch; the per-step inputs and outputs
-    // above are then [ksteps, n, ...] arrays, step-major (step t at offset t * n * width)
+    // above are then [ksteps, n, ...] arrays, step-major: lane i's row of step t is io = t * n + i
     int ksteps;
 };
-
-// the inputs / outputs of step t of a multi-step launch (NULL stays NULL)
-__device__ inline KArgs step_args(const KArgs& a, int t) {
-    if (t == 0) return a;
-    KArgs s = a;
-    const long o = (long)t * a.n;
-    auto off = [o](auto* p, int w) { return p ? p + o * w : p; };
-    s.act = off(a.act, HUM_NACT);
-    s.obs = off(a.obs, HUM_NOBS);
-    s.rew = off(a.rew, 1);
-    s.done = off(a.done, 1);
-    s.frame_out = off(a.frame_out, 1);
-    s.obs_reset = off(a.obs_reset, HUM_NOBS);
-    s.act_high = off(a.act_high, HUM_NACT_HIGH);
-    s.agent_sel = off(a.agent_sel, 1);
-    s.agents = off(a.agents, 1);
-    s.obs_high = off(a.obs_high, HUM_NOBS_HIGH);
-    s.rew_high = off(a.rew_high, 1);
-    s.obs_high_reset = off(a.obs_high_reset, HUM_NOBS_HIGH);
-    return s;
-}
 
 // CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
 // np.clip(a, -1, 1)) - a float32 product under NumPy >= 2 (NEP 50), float64 under NumPy 1.x
@@ -252,8 +231,11 @@ __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i,
 
 // Post-physics part of step (low_level_env.py:481-526) + optional auto-reset; stores state, book, outputs.
 template <typename T>
-__device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, T* st, Book& b, const float* act, unsigned& ef, const T* scs = nullptr,
-                          bool* defer_reset = nullptr) {   // defer_reset: the caller runs the auto-reset and the store
+__device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, long io, T* st, Book& b, const float* act,
+                                                          unsigned& ef, const T* scs = nullptr,
+                                                          bool* defer_reset = nullptr) {   // defer_reset: the caller
+                                                                                           // runs the auto-reset and the store
+    // i: the lane (state, bookkeeping); io: its output row of this step (t * n + i, hum_step_k)
     const ClipDev& c = a.clips[b.clip];
     float obs[HUM_NOBS];
     // calc_state (:481) and robot_pos (:483-486)
@@ -325,10 +307,10 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         if (b.timestep >= 3000) done = true;
     }
 #pragma unroll
-    for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = obs[k];
-    a.rew[i] = (float)total;
-    a.done[i] = done ? 1 : 0;
-    if (a.frame_out) a.frame_out[i] = b.frame;
+    for (int k = 0; k < HUM_NOBS; k++) a.obs[io * HUM_NOBS + k] = obs[k];
+    a.rew[io] = (float)total;
+    a.done[io] = done ? 1 : 0;
+    if (a.frame_out) a.frame_out[io] = b.frame;
     if (defer_reset) {
         *defer_reset = done && (a.flags & HUM_STEP_AUTORESET);
         return;
@@ -338,7 +320,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         reset_lane(a, i, st, b, -1, 0.0, o2, ef);
         if (a.obs_reset) {
 #pragma unroll
-            for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[(long)i * HUM_NOBS + k] = o2[k];
+            for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[io * HUM_NOBS + k] = o2[k];
         }
     }
     store_lane(a, i, st, b);
@@ -451,7 +433,8 @@ __device__ inline float hier_update_reward_high(Book& b) {
 // step(action_dict) (hier_env.py:355-366) -> high_level_step (:538-571) or low_level_step (:583-641), after the
 // physics of a low step; stores state/book and writes the dict-shaped outputs.
 template <typename T>
-__device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, T* st, Book& b, bool high, unsigned& ef, const T* scs = nullptr) {
+__device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, long io, T* st, Book& b, bool high, unsigned& ef,
+                                                          const T* scs = nullptr) {
     const ClipDev& c = a.clips[b.clip];
     b.robot_pos[0] = b.bxy[0]; b.robot_pos[1] = b.bxy[1]; b.robot_pos[2] = 0;   // step(): :358-361
     float obs[HUM_NOBS], js[NDOF], o44[HUM_NOBS_HIGH];
@@ -463,7 +446,7 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     if (high) {
         // cur_obs is the last calc_state (same physics state, walk target before this call)
         calc_state(st, b.wt, obs, js, jal, pp);
-        const float a0 = a.act_high[2 * (long)i], a1 = a.act_high[2 * (long)i + 1];
+        const float a0 = a.act_high[2 * io], a1 = a.act_high[2 * io + 1];
         const float actionDegree = (float)atan2((double)a1, (double)a0) * (float)RAD2DEG;   // :540 (float32)
         const double newDegree = (double)actionDegree + pp.yaw * RAD2DEG;                   // :543
         b.hldt = newDegree * DEG2RAD;
@@ -484,7 +467,7 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     } else {
         b.level_rem -= 1;                                                                   // :584
         calc_state(st, b.wt, obs, js, jal, pp, scs);                                        // :591
-        const float* act = a.act + (long)i * HUM_NACT;
+        const float* act = a.act + io * HUM_NACT;
         // updateReward (:494-522)
         double dJ = 0, dV = 0;
 #pragma unroll
@@ -567,23 +550,23 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     }
     if (agents & HUM_AGENT_LOW) {
 #pragma unroll
-        for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = obs[k];
+        for (int k = 0; k < HUM_NOBS; k++) a.obs[io * HUM_NOBS + k] = obs[k];
     }
     if (agents & HUM_AGENT_HIGH) {
 #pragma unroll
-        for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high[(long)i * HUM_NOBS_HIGH + k] = o44[k];
+        for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high[io * HUM_NOBS_HIGH + k] = o44[k];
     }
-    a.rew[i] = (agents & HUM_AGENT_LOW) ? rew_low : 0.f;   // the level hand-back drops the low reward (:631-636)
-    a.rew_high[i] = rew_high;
-    a.agents[i] = (unsigned char)agents;
-    a.done[i] = done ? 1 : 0;
-    if (a.frame_out) a.frame_out[i] = b.frame;
+    a.rew[io] = (agents & HUM_AGENT_LOW) ? rew_low : 0.f;   // the level hand-back drops the low reward (:631-636)
+    a.rew_high[io] = rew_high;
+    a.agents[io] = (unsigned char)agents;
+    a.done[io] = done ? 1 : 0;
+    if (a.frame_out) a.frame_out[io] = b.frame;
     if (done && (a.flags & HUM_STEP_AUTORESET)) {
         float r44[HUM_NOBS_HIGH];
         hier_reset_lane(a, i, st, b, -1, 0.0, r44, ef);
         if (a.obs_high_reset) {
 #pragma unroll
-            for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high_reset[(long)i * HUM_NOBS_HIGH + k] = r44[k];
+            for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high_reset[io * HUM_NOBS_HIGH + k] = r44[k];
         }
     }
     store_lane(a, i, st, b);
@@ -591,16 +574,16 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
 }
 
 // non-finite action on a lane (humanoid.py:55 assert): lane not stepped, flagged, outputs neutral
-__device__ inline void nonfinite_outputs(const KArgs& a, int i, int frame) {
+__device__ inline void nonfinite_outputs(const KArgs& a, long io, int frame) {
     if (!a.hier) {
-        for (int k = 0; k < HUM_NOBS; k++) a.obs[(long)i * HUM_NOBS + k] = 0.f;
+        for (int k = 0; k < HUM_NOBS; k++) a.obs[io * HUM_NOBS + k] = 0.f;
     } else {
-        a.rew_high[i] = 0.f;
-        a.agents[i] = 0;
+        a.rew_high[io] = 0.f;
+        a.agents[io] = 0;
     }
-    a.rew[i] = 0.f;
-    a.done[i] = 1;
-    if (a.frame_out) a.frame_out[i] = frame;
+    a.rew[io] = 0.f;
+    a.done[io] = 1;
+    if (a.frame_out) a.frame_out[io] = frame;
 }
 
 #pragma clang fp contract(on)
@@ -608,33 +591,33 @@ __device__ inline void nonfinite_outputs(const KArgs& a, int i, int frame) {
 
 // ----------------------------------------------------------------------------------- step
 template <typename T>
-__global__ void __launch_bounds__(256) step_kernel(KArgs a0) {
+__global__ void __launch_bounds__(256) step_kernel(KArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a0.n) return;
+    if (i >= a.n) return;
     T st[HUM_NSTATE];
     Book b;
-    load_lane(a0, i, st, b);
+    load_lane(a, i, st, b);
     unsigned ef = 0;
 #pragma unroll 1
-    for (int t = 0; t < a0.ksteps; t++) {   // env steps of this launch (state and book stay in registers)
-        const KArgs a = step_args(a0, t);
+    for (int t = 0; t < a.ksteps; t++) {   // env steps of this launch (state and book stay in registers)
+        const long io = (long)t * a.n + i;
         // hierarchical env: the lane's acting agent (step(action_dict) dispatch, hier_env.py:363-366); a lane with
         // no action this round (HUM_AGENT_SEL_SKIP) is left untouched and reports no agent
-        if (a.hier && a.agent_sel && a.agent_sel[i] == HUM_AGENT_SEL_SKIP) {
-            a.agents[i] = 0;
+        if (a.hier && a.agent_sel && a.agent_sel[io] == HUM_AGENT_SEL_SKIP) {
+            a.agents[io] = 0;
             continue;
         }
-        const bool high = a.hier && (a.agent_sel ? a.agent_sel[i] != 0 : b.expect_high != 0);
+        const bool high = a.hier && (a.agent_sel ? a.agent_sel[io] != 0 : b.expect_high != 0);
         float act[HUM_NACT];
         bool finite = true;
 #pragma unroll
         for (int k = 0; k < HUM_NACT; k++) {
-            act[k] = a.act[(long)i * HUM_NACT + k];
+            act[k] = a.act[io * HUM_NACT + k];
             finite &= isfinite(act[k]);
         }
         if (!finite && !high) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
-            nonfinite_outputs(a, i, b.frame);
+            nonfinite_outputs(a, io, b.frame);
             continue;
         }
         if (!(a.flags & HUM_STEP_SKIP_PHYSICS) && !high) {
@@ -649,10 +632,10 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a0) {
             }
         }
         unsigned ef1 = 0;   // hier_post / post_step publish their own flags
-        if (a.hier) hier_post(a, i, st, b, high, ef1);
-        else post_step(a, i, st, b, act, ef1);
+        if (a.hier) hier_post(a, i, io, st, b, high, ef1);
+        else post_step(a, i, io, st, b, act, ef1);
     }
-    if (ef) atomicOr(a0.eflags, ef);
+    if (ef) atomicOr(a.eflags, ef);
 }
 
 // Cooperative step: 16 lanes per env, EPB_ envs per block of EPB_*16 threads (one wavefront), env working
@@ -664,15 +647,12 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a0) {
 template <typename T, int EPB_, bool TERRAIN = false>
 __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a0) {
     __shared__ GroupLDS<T> sh[EPB_];
-    const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL;
+    const int ksteps = a0.ksteps;
     // XCD-aware env mapping: the dispatcher deals blocks round-robin over the 8 XCDs (block b -> XCD b % 8),
     // so consecutive blocks would put the 4-env (16/32-byte) slices of one SoA cache line into 8 different L2s,
     // each fetching the whole line.  Give XCD x one contiguous run of blocks instead (a bijection for any grid).
     const int nb = gridDim.x, xq = nb >> 3, xr = nb & 7, xcd = blockIdx.x & 7;
     const int blk = xcd * xq + min(xcd, xr) + (blockIdx.x >> 3);
-    const int i = blk * EPB_ + ge;
-    const bool valid = i < a0.n;
-    GroupLDS<T>& S = sh[ge];
 #ifdef HUM_WLOG_ON
     const unsigned long long t_wave0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt_wave0 = __builtin_amdgcn_s_memrealtime();
@@ -681,32 +661,50 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
 #endif
 #endif
     load_tab_lds<T>();
-    const ModelTab<T>& M = tab<T>();
-    // the env's state stays in LDS over the steps of the launch; lane 0 carries the per-env integers the other
-    // lanes read (the agent the hierarchical env expects, the random-terrain key) in the pad slots of tau
-    for (int e = l; e < HUM_NSTATE; e += GL)
-        S.st[e] = valid ? ((const T*)a0.phys)[(long)e * a0.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
-    static_assert(sizeof(T) * 3 >= 3 * sizeof(int), "carry slots");
-    int* carry = reinterpret_cast<int*>(&S.tau[NDOF]);
-    if (l == 0) {
-        carry[0] = valid && a0.hier ? a0.bi[10 * a0.n + i] : 0;
-        carry[1] = TERRAIN && a0.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid ? a0.bi[11 * a0.n + i] : 0;
-        carry[2] = TERRAIN && a0.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid ? a0.bi[12 * a0.n + i] : 0;
+    {   // the env's state stays in LDS over the steps of the launch; lane 0 carries the per-env integers the other
+        // lanes read (the agent the hierarchical env expects, the random-terrain key) in the pad slots of tau
+        const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL, i = blk * EPB_ + ge;
+        const bool valid = i < a0.n;
+        GroupLDS<T>& S = sh[ge];
+        for (int e = l; e < HUM_NSTATE; e += GL)
+            S.st[e] = valid ? ((const T*)a0.phys)[(long)e * a0.n + i] : (e == 2 ? T(1.17) : (e == 6 ? T(1) : T(0)));
+        static_assert(sizeof(T) * 3 >= 3 * sizeof(int), "carry slots");
+        int* carry = reinterpret_cast<int*>(&S.tau[NDOF]);
+        if (l == 0) {
+            carry[0] = valid && a0.hier ? a0.bi[10 * a0.n + i] : 0;
+            carry[1] = TERRAIN && a0.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid ? a0.bi[11 * a0.n + i] : 0;
+            carry[2] = TERRAIN && a0.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid ? a0.bi[12 * a0.n + i] : 0;
+        }
     }
     __syncthreads();
     unsigned ef = 0;
-    const int gbit = (threadIdx.x & 63) & ~(GL - 1);
 #pragma unroll 1
-    for (int t = 0; t < a0.ksteps; t++) {
-    const KArgs a = step_args(a0, t);
+    for (int t = 0; t < ksteps; t++) {
+    // Everything the step body derives from the launch arguments or the lane index is recomputed in every step:
+    // the arguments are re-read from the kernarg segment and the lane index is laundered, so the compiler cannot
+    // hoist those values out of the step loop (which would keep them live across the whole body and spill).
+    const __attribute__((address_space(4))) KArgs* kp =
+        (const __attribute__((address_space(4))) KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    const KArgs& a = *(const KArgs*)kp;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int l = tid & (GL - 1), ge = tid / GL;
+    const int i = blk * EPB_ + ge;
+    const bool valid = i < a.n;
+    GroupLDS<T>& S = sh[ge];
+    const ModelTab<T>& M = tab_fresh<T>();
+    int* carry = reinterpret_cast<int*>(&S.tau[NDOF]);
+    const int gbit = (tid & 63) & ~(GL - 1);
+    const long io = (long)t * a.n + i;   // this step's input / output row of the env
     bool fin = true;
     for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60)
-        const float av = valid ? a.act[(long)i * HUM_NACT + k] : 0.f;
+        const float av = valid ? a.act[io * HUM_NACT + k] : 0.f;
         fin = fin && isfinite(av);
         S.tau[M.act_dof[k]] = (T)motor_torque(a.np1, M.act_gain[k], M.act_gain_d[k], isfinite(av) ? av : 0.f);
     }
     // hierarchical env: envs whose acting agent is the high level take no physics step (hier_env.py:538-571)
-    const unsigned char sel = a.hier && valid && a.agent_sel ? a.agent_sel[i] : (unsigned char)0;
+    const unsigned char sel = a.hier && valid && a.agent_sel ? a.agent_sel[io] : (unsigned char)0;
     const bool skip = a.hier && valid && a.agent_sel && sel == HUM_AGENT_SEL_SKIP;   // no action: lane untouched
     const bool high = a.hier && valid && !skip && (a.agent_sel ? sel != 0 : carry[0] != 0);
     const bool env_ok = high || ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
@@ -735,13 +733,13 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     T st[HUM_NSTATE];
     bool rst = false, stored = false;
     if (valid && l == 0 && skip) {
-        a.agents[i] = 0;
+        a.agents[io] = 0;
     } else if (valid && l == 0) {
         load_book(a, i, b);
         SUBPHASE(17);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
-            nonfinite_outputs(a, i, b.frame);
+            nonfinite_outputs(a, io, b.frame);
         } else {
             if (high) {   // physics (if the wave ran it) is discarded: the HBM state is the current one
 #pragma unroll
@@ -751,13 +749,13 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
                 for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
             }
             if (a.hier) {
-                hier_post(a, i, st, b, high, ef, high ? nullptr : scs);   // high: the HBM state, not S.st
+                hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs);   // high: the HBM state, not S.st
                 stored = true;
             } else {
                 float act[HUM_NACT];
 #pragma unroll
-                for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[(long)i * HUM_NACT + k];
-                post_step(a, i, st, b, act, ef, scs, &rst);
+                for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[io * HUM_NACT + k];
+                post_step(a, i, io, st, b, act, ef, scs, &rst);
             }
         }
     }
@@ -797,7 +795,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
                 reset_lane(a, i, st, b, sf, 0.0, o2, ef, scs_r);
                 if (a.obs_reset) {
 #pragma unroll
-                    for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[(long)i * HUM_NOBS + k] = o2[k];
+                    for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[io * HUM_NOBS + k] = o2[k];
                 }
             }
             store_lane(a, i, st, b);
@@ -805,7 +803,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         }
     }
     PHASE(10);
-    if (a0.ksteps > 1) {   // wave-uniform: publish the env's state for the next step of this launch
+    if (a.ksteps > 1) {   // wave-uniform: publish the env's state for the next step of this launch
         if (valid && l == 0) {
             if (!stored) {   // not stepped (no action / non-finite action): the stored state stands
 #pragma unroll

@@ -261,6 +261,19 @@ template <> __device__ inline const ModelTab<float>& tab<float>() { return sTabF
 template <> __device__ inline const ModelTab<float>& tab<float>() { return kTabF; }
 #endif
 template <> __device__ inline const ModelTab<double>& tab<double>() { return kTabD; }
+// The table through a pointer the compiler cannot see through: its constant-offset loads are then issued where they
+// are used (scalar loads) instead of being hoisted out of the substep / step loops into registers live across them.
+template <typename T>
+__device__ __attribute__((always_inline)) inline const ModelTab<T>& tab_fresh() {
+#ifdef HUM_TAB_LDS
+    return tab<T>();
+#else
+    using CT = const __attribute__((address_space(4))) ModelTab<T>;
+    CT* p = (CT*)&tab<T>();
+    asm volatile("" : "+s"(p));
+    return *(const ModelTab<T>*)p;
+#endif
+}
 
 template <typename T>
 __device__ inline void load_tab_lds() {   // block-wide; the caller's __syncthreads publishes it
@@ -693,7 +706,7 @@ __device__ inline void pgs_link(int epos, int q, int nl, int nc, int& next3, int
 template <typename T, int EPB_>
 __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, GroupLDS<T>* shb, T* gblock, int nl, int nc,
                                                           const T dt, int& pbase, int& ptot) {
-    const ModelTab<T>& M = tab<T>();
+    const ModelTab<T>& M = tab_fresh<T>();
     const int lane = threadIdx.x & 63, cap = P.lds_rows;
     const T idt = T(1) / dt;
     // pre: task prefix (actual rows); pos: pool prefix (short envs are padded with zero rows, see PGS)
@@ -1021,7 +1034,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                                                              T* gblock, const int l, unsigned& ef,
                                                              unsigned long long tkey) {   // tkey: terrain 2
     GroupLDS<T>& S = shb[ge];
-    const ModelTab<T>& M = tab<T>();
+    const ModelTab<T>& M = tab_fresh<T>();
     const T dt = (T)P.dt;
     PHASE_INIT;
     // ---- FK (every lane, registers); lane 0 publishes

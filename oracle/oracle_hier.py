@@ -58,6 +58,34 @@ class OracleHierEnv:
         self.cur_obs = np.zeros(42, dtype=np.float32)
         self.initReward()
 
+    @classmethod
+    def from_lane(cls, clip, phys, book, bk, numpy_semantics=O.DEFAULT_NUMPY):
+        """An env holding exactly one product lane's state (hum_get_state rows; bk = the HUM_BK_* column map, passed
+        in: the oracle imports nothing from the product).  cur_obs is the calc_state of that state under the lane's
+        walk target, which is what the reference holds between calls (its walk target changes only in
+        high_level_step and resetFromFrame, after which cur_obs is not recomputed until the next low step)."""
+        o = cls(clip, numpy_semantics=numpy_semantics)
+        o.state = np.array(phys, dtype=np.float64).copy()
+        o.selected_motion_frame = int(book[bk["frame"]])
+        o.cur_timestep = int(book[bk["cur_timestep"]])
+        o.predefinedTargetIndex = int(book[bk["predefinedTargetIndex"]])
+        for k in ("target", "starting_robot_pos", "robot_pos", "starting_ep_pos"):
+            setattr(o, k, np.array(book[bk[k]:bk[k] + 3], dtype=np.float64))
+        o.walk_target = (float(book[bk["walk_target"]]), float(book[bk["walk_target"] + 1]))
+        o.highLevelDegTarget = float(book[bk["highLevelDegTarget"]])
+        for k in ("lowTargetScore", "deltaJoints", "deltaVelJoints", "bodyPostureScore", "electricityScore",
+                  "jointLimitScore", "aliveReward", "delta_lowTargetScore", "highTargetScore", "driftScore",
+                  "cumulative_driftScore", "delta_highTargetScore", "cumulative_aliveReward"):
+            setattr(o, k, float(book[bk[k]]))
+        o.steps_remaining_at_level = int(book[bk["steps_remaining_at_level"]])
+        o.num_high_level_steps = int(book[bk["num_high_level_steps"]])
+        o.body_xyz = (float(book[bk["body_xy"]]), float(book[bk["body_xy"] + 1]), float(phys[2]))
+        key = int(book[bk["rng_key_lo"]]) | (int(book[bk["rng_key_hi"]]) << 32)
+        o.rng = O.LaneRNG(key=key, counter=int(book[bk["rng_counter"]]))
+        obs, _, js, jal, _ = O.calc_state(o.state, o.walk_target)
+        o.cur_obs, o.joint_speeds, o.joints_at_limit = obs, js, jal
+        return o
+
     def initReward(self):                                           # :183-206
         self.deltaJoints = 0
         self.deltaVelJoints = 0

@@ -187,6 +187,9 @@ def test_hier_host_io_equals_device_path():
         np.testing.assert_array_equal(done, dev[5])
     p0, b0 = envs[0].get_state()
     p1, b1 = envs[1].get_state()
+    inv = {v: k for k, v in N.BK.items()}
+    for i, c in np.argwhere(b0 != b1)[:10]:
+        print("lane %d book %d (%s): %r vs %r" % (i, c, inv.get(c), b0[i, c], b1[i, c]))
     np.testing.assert_array_equal(p0, p1)
     np.testing.assert_array_equal(b0, b1)
     for e in envs:

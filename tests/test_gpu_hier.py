@@ -237,3 +237,33 @@ def test_hier_gym_view_and_base_env():
             acts[i] = {HIGH: np.array([0.0, 1.0], np.float32)} if HIGH in o and LOW not in o or dones[i]["__all__"] \
                 else {LOW: np.zeros(17, np.float32)}
     v.stop()
+
+
+@pytest.mark.parametrize("name", HIER_SCEN)
+def test_hier_physics_fp32_matches_oracle(golden_hier, name):
+    """The benchmarked fp32 kernel with full physics on the golden two-level scenarios vs the fp64 oracle physics
+    (one call each from the recorded state): the fp32 step bound of the configs 2 / 3 / 5 scale tests on every
+    well-conditioned low-level call (oracle obs moving by <= 1e-5 under a 2^-24 relative input perturbation),
+    agents / done / frame / counters exact there."""
+    from test_gpu_scale import FP32_BOUND, SENS_BOUND
+    r = rec(golden_hier, name)
+    o = run_scenario(r, "fp32", skip_physics=False, kernel=1)
+    hl = r["has_low"].astype(bool)
+    low_call = r["agent"] == 0
+    rng = np.random.default_rng(1)
+    good = np.ones(len(r["done"]), bool)
+    for t in np.nonzero(low_call)[0]:
+        tau = O.motor_torques(r["action_low"][t].astype(np.float32), O.NUMPY_2)
+        wt = tuple(r["book_walk_target"][t])
+        ref = O.calc_state(O.phys_step(r["state_pre"][t], tau), wt)[0]
+        pert = O.calc_state(O.phys_step(r["state_pre"][t] * (1 + 2.0 ** -24 * rng.choice([-1.0, 1.0], 47)), tau), wt)[0]
+        good[t] = np.abs(pert - ref).max() <= SENS_BOUND
+    assert good.sum() >= 0.8 * len(good)
+    np.testing.assert_array_equal(o["done"][good], r["done"][good])
+    np.testing.assert_array_equal(o["frame"][good], r["book_selected_motion_frame"][good].astype(np.int32))
+    m = hl & good
+    err = np.abs(o["ol"][m] - r["obs_low"][m]).max(initial=0)
+    print("%s: fp32 low obs max %.3g over %d conditioned calls (%d ill-conditioned)" % (name, err, m.sum(),
+                                                                                       (~good).sum()))
+    assert err <= FP32_BOUND["obs_max"]
+    np.testing.assert_allclose(o["rl"][good], r["rew_low"][good], rtol=0, atol=FP32_BOUND["reward_max"])

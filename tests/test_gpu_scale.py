@@ -1,9 +1,12 @@
-"""GPU parity at the benchmark's full size (BASELINE configs 2 and 3) and on contact-heavy states.
+"""GPU parity at the benchmark's full size (BASELINE configs 2, 3 and 5) and on contact-heavy states.
 
 * 4096 lanes x 200 auto-reset steps of config 2 (motion02_04) and config 3 (the four clips round-robin per
   lane), uniform random actions: no contact is ever dropped (HUM_EFLAG_CONTACT_OVERFLOW stays clear), and a
   sample of 64 lanes per clip, taken mid-rollout, steps exactly like the oracle (oracle.phys_step + the oracle
   env logic, low_level_env.py:475-526) from the lane's injected state, bookkeeping and RNG stream.
+* config 5 (the two-level env, hier_env.py:355-366, 538-642): 4096 lanes x 200 auto-reset agent transitions,
+  then 64 lanes whose next transition is a high-level one and 64 whose next is a low-level (physics) one step
+  once more on the GPU and in oracle_hier.OracleHierEnv from the injected state, bookkeeping and RNG stream.
 * contact-heavy states (>= 17 contacts: past the 16 the cooperative kernel keeps in LDS) step like the oracle,
   so the global contact spill path is exact; a lowered max_contacts still flags its overflow.
 
@@ -19,6 +22,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+import oracle_hier as OH
 from oracle_inject import BK, contact_heavy_states, oracle_from_lane
 
 pytestmark = pytest.mark.gpu
@@ -33,14 +37,19 @@ from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
 # one fp32 env step vs the fp64 oracle from the same state ("fp32 step bound"): float32
 # rounding through 4 substeps of dynamics and the contact / limit solve; measured over the sampled lanes (obs
-# max 3.4e-5, reward max 1.7e-6, no done flips; profiles/r02_parity_scale_*.json), bound with margin
-FP32_BOUND = {"obs_max": 2.5e-4, "reward_max": 1e-5}
+# max 3.4e-5 - 5.1e-5 conditioned, reward max 1.7e-6, no done flips; profiles/r02_parity_scale_*.json,
+# profiles/r03_*), bound 2x the worst measured
+FP32_BOUND = {"obs_max": 1e-4, "reward_max": 1e-5}
 # Conditioning: a lane whose oracle step moves its obs by more than SENS_BOUND when the input state is perturbed by
 # 2^-24 relative (float32 rounding) sits at a discontinuity of the model (a joint limit or contact switching on within
 # that margin; Bullet's limits and contacts act only when violated / within the threshold).  There float32 vs float64
 # rounding inside the step can switch it too, so the error is the model's; such lanes are counted, not bounded.
 SENS_BOUND = 1e-5
-MAX_ILL_FRACTION = 0.25   # measured 8 / 64 (config 2, 200 random-action steps: joints resting on their limits)
+# measured 4 - 10 of 64 per clip sample (joints resting on their limits after 200 random-action steps); every
+# excluded lane is checked instead through the fp64 kernel stepped from the identical state (FP64_BOUND): the
+# exclusion is the model's discontinuity, not the fp32 kernel's
+MAX_ILL_FRACTION = 0.2
+FP64_BOUND = {"obs_max": 1e-5, "reward_max": 1e-5, "state_max": 1e-6}
 
 
 def _sample_lanes(book, c, name, per_clip, n):
@@ -63,7 +72,14 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
     obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
     phys2, book2 = env.get_state()
     env.close()
-    st = {"obs": [], "rew": [], "done": [], "state": [], "sens": [], "frame_ok": True, "lanes": 0}
+    # the fp64 kernel from the identical state (checks the lanes the fp32 bound excludes)
+    env64 = HumanoidVecEnv(n, clips=clips, seed=seed, precision="fp64")
+    env64.set_state(phys, book)
+    obs64, rew64, done64, _ = [x.cpu().numpy() for x in env64.step(torch.as_tensor(a, device="cuda"))]
+    phys64, _ = env64.get_state()
+    env64.close()
+    st = {"obs": [], "rew": [], "done": [], "state": [], "sens": [], "frame_ok": True, "lanes": 0,
+          "obs64": [], "rew64": [], "done64": [], "state64": []}
     prng = np.random.default_rng(6)
     for c, name in enumerate(clips):
         clip = load_clip(name)
@@ -74,6 +90,10 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
             st["rew"].append(abs(float(rew[i]) - rr))
             st["done"].append(bool(done[i]) != rd)
             st["state"].append(np.abs(phys2[i] - o.state).max())
+            st["obs64"].append(np.abs(obs64[i] - ro).max())
+            st["rew64"].append(abs(float(rew64[i]) - rr))
+            st["done64"].append(bool(done64[i]) != rd)
+            st["state64"].append(np.abs(phys64[i] - o.state).max())
             p = oracle_from_lane(clip, phys[i] * (1 + 2.0 ** -24 * prng.choice([-1.0, 1.0], 47)), book[i])
             st["sens"].append(np.abs(p.step(a[i])[0] - ro).max())
             st["frame_ok"] &= int(frame[i]) == o.frame and int(book2[i, BK["cur_timestep"]]) == o.cur_timestep
@@ -91,6 +111,10 @@ def _summary(tag, st):
          "ill_conditioned": int((~good).sum()), "obs_max_conditioned": float(st["obs"][good].max()),
          "reward_max_conditioned": float(st["rew"][good].max()),
          "done_mismatch_conditioned": int(st["done"][good].sum()), "sens_max": float(st["sens"].max())}
+    if "obs64" in st and len(st["obs64"]):
+        s["fp64_kernel_same_state"] = {"obs_max": float(st["obs64"].max()), "reward_max": float(st["rew64"].max()),
+                                       "state_max": float(st["state64"].max()), "done_mismatch": int(st["done64"].sum()),
+                                       "obs_max_ill_conditioned": float(st["obs64"][~good].max(initial=0))}
     print(tag, json.dumps(s))
     out = os.environ.get("ILRL_PARITY_OUT")
     if out:
@@ -114,10 +138,17 @@ def test_full_size_rollout_no_drop_and_sample_matches_oracle(config, precision):
         assert s["obs_max"] < 1e-5 and s["reward_max"] < 1e-5
         assert s["done_mismatch"] == 0
     else:
-        assert s["obs_max_conditioned"] <= FP32_BOUND["obs_max"]
-        assert s["reward_max_conditioned"] <= FP32_BOUND["reward_max"]
-        assert s["done_mismatch_conditioned"] == 0
-        assert s["ill_conditioned"] <= MAX_ILL_FRACTION * s["lanes"]
+        _check_fp32(s)
+
+
+def _check_fp32(s):
+    assert s["obs_max_conditioned"] <= FP32_BOUND["obs_max"]
+    assert s["reward_max_conditioned"] <= FP32_BOUND["reward_max"]
+    assert s["done_mismatch_conditioned"] == 0
+    assert s["ill_conditioned"] <= MAX_ILL_FRACTION * s["lanes"]
+    f64 = s["fp64_kernel_same_state"]   # every lane incl. the excluded ones: the model, not the kernel
+    assert f64["obs_max"] <= FP64_BOUND["obs_max"] and f64["reward_max"] <= FP64_BOUND["reward_max"]
+    assert f64["state_max"] <= FP64_BOUND["state_max"] and f64["done_mismatch"] == 0
 
 
 @pytest.mark.parametrize("kernel", [1, 0])
@@ -151,3 +182,98 @@ def test_lowered_contact_cap_flags_overflow():
     env.step(torch.zeros(8, 17, device="cuda"))
     assert env.error_flags() & N.HUM_EFLAG_CONTACT_OVERFLOW
     env.close()
+
+
+# ------------------------------------------------------------------------------------------ config 5 (hier)
+def _agents_of(robs):
+    return (N.HUM_AGENT_HIGH if OH.HIGH in robs else 0) | (N.HUM_AGENT_LOW if OH.LOW in robs else 0)
+
+
+def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23):
+    from ilrl_amd.hier_env import HierVecEnv, HIER_CLIP
+    clip = load_clip(HIER_CLIP)
+    env = HierVecEnv(n, seed=seed, precision=precision)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for _ in range(steps):
+        env.step(torch.rand(n, 2, device="cuda", generator=g) * 2 - 1,
+                 torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
+    flags = env.error_flags()
+    phys, book = env.get_state()
+    rng = np.random.default_rng(15)
+    ah = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+    al = rng.uniform(-1, 1, (n, 17)).astype(np.float32)
+    T = lambda x: torch.as_tensor(x, device="cuda")
+    outs = {}
+    for prec, e in ((precision, env), ("fp64", None)):
+        if e is None:   # the fp64 kernel from the identical state
+            e = HierVecEnv(n, seed=seed, precision="fp64")
+            e.set_state(phys, book)
+        res = [x.cpu().numpy() for x in e.step(T(ah), T(al))]
+        outs[prec if e is env else "f64"] = res + list(e.get_state())
+        e.close()
+    agents, oh, ol, rh, rl, done, frame, phys2, book2 = outs[precision]
+    a64, oh64, ol64, rh64, rl64, d64, _, p64, _ = outs["f64"]
+    expect = book[:, BK["expect_high"]].astype(int)
+    st = {k: [] for k in ("obs", "rew", "done", "state", "sens", "obs64", "rew64", "done64", "state64", "kind")}
+    st["exact_ok"], st["lanes"] = True, 0
+    prng = np.random.default_rng(16)
+    for kind in (1, 0):   # high-level transition, low-level (physics) transition
+        lanes = np.nonzero(expect == kind)[0]
+        assert len(lanes) >= per_kind
+        for i in lanes[np.linspace(0, len(lanes) - 1, per_kind).astype(int)]:
+            act = {OH.HIGH: ah[i]} if kind else {OH.LOW: al[i]}
+            o = OH.OracleHierEnv.from_lane(clip, phys[i], book[i], BK)
+            robs, rrew, rdone, _ = o.step(act)
+            ag = _agents_of(robs)
+            st["exact_ok"] &= int(agents[i]) == ag and int(a64[i]) == ag
+            st["exact_ok"] &= int(frame[i]) == o.selected_motion_frame
+            for k, v in (("cur_timestep", o.cur_timestep), ("rng_counter", o.rng.counter),
+                         ("steps_remaining_at_level", o.steps_remaining_at_level),
+                         ("num_high_level_steps", o.num_high_level_steps)):
+                st["exact_ok"] &= int(book2[i, BK[k]]) == int(v)
+
+            def errs(obs_h, obs_l, r_h, r_l):
+                e = 0.0
+                if OH.HIGH in robs:
+                    e = max(e, float(np.abs(obs_h[i] - robs[OH.HIGH]).max()))
+                if OH.LOW in robs:
+                    e = max(e, float(np.abs(obs_l[i] - robs[OH.LOW]).max()))
+                r = max(abs(float(r_h[i]) - float(rrew.get(OH.HIGH, 0))), abs(float(r_l[i]) - float(rrew.get(OH.LOW, 0))))
+                return e, r
+            eo, er = errs(oh, ol, rh, rl)
+            eo64, er64 = errs(oh64, ol64, rh64, rl64)
+            st["obs"].append(eo)
+            st["rew"].append(er)
+            st["done"].append(bool(done[i]) != rdone["__all__"])
+            st["state"].append(float(np.abs(phys2[i] - o.state).max()))
+            st["obs64"].append(eo64)
+            st["rew64"].append(er64)
+            st["done64"].append(bool(d64[i]) != rdone["__all__"])
+            st["state64"].append(float(np.abs(p64[i] - o.state).max()))
+            if kind:
+                st["sens"].append(0.0)   # no physics: no discontinuity
+            else:
+                p = OH.OracleHierEnv.from_lane(clip, phys[i] * (1 + 2.0 ** -24 * prng.choice([-1.0, 1.0], 47)), book[i],
+                                               BK)
+                pobs = p.step(act)[0]
+                st["sens"].append(max(float(np.abs(pobs[k] - robs[k]).max()) for k in robs if k in pobs))
+            st["kind"].append(kind)
+            st["lanes"] += 1
+    return flags, {k: (np.array(v) if isinstance(v, list) else v) for k, v in st.items()}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_hier_full_size_rollout_sample_matches_oracle(precision):
+    """Config 5 at full size: 4096 lanes, 200 auto-reset transitions, then 64 high-level and 64 low-level
+    transitions vs the oracle from the injected lane state (hier_env.py:355-366, 538-642)."""
+    flags, st = hier_rollout_and_compare(precision)
+    assert flags & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
+    assert st["exact_ok"], "agents / frame / timestep / RNG counter / level counters differ from the oracle"
+    s = _summary("c5_%s" % precision, st)
+    if precision == "fp64":
+        assert s["state_max"] < FP64_BOUND["state_max"]
+        assert s["obs_max"] < FP64_BOUND["obs_max"] and s["reward_max"] < FP64_BOUND["reward_max"]
+        assert s["done_mismatch"] == 0
+    else:
+        _check_fp32(s)
