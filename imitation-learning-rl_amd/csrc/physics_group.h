@@ -39,7 +39,8 @@ static_assert(limits_proper(), "a dof with lo >= hi could violate both sides");
 constexpr int MAXR_G = NDOF + 3 * MAXC_G;    // rows of one env: limits + (normal + 2 frictions) per contact
 // constraint row layout (T units): J and M^-1 J^T interleaved per dof ([2q] = J_q, [2q+1] = (M^-1 J^T)_q), a
 // zero pair (read by the lanes without a second velocity component), then two 16-byte scalar quads:
-// b, hi, lambda, 1/(J M^-1 J^T) and mu, c = J . (M^-1 J^T of the predecessor row), next3, next3_ln (ints).
+// b, hi, lambda, meff = 1/(J M^-1 J^T) and mu, q = meff * J . (M^-1 J^T of the predecessor row), next3, next3_ln
+// (ints).
 // lo is 0 for every row type and not stored.
 constexpr int RO_Z = 2 * NV;          // zero pair
 constexpr int RO_S0 = 2 * NV + 2;     // b, hi, lam, meff
@@ -849,7 +850,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 T c = 0;
 #pragma unroll
                 for (int q = 0; q < NV; q++) c += Rr[2 * q] * Rp[2 * q + 1];
-                Rr[RO_S1 + 1] = c;
+                Rr[RO_S1 + 1] = c * Rr[RO_S0 + 3];   // q_r = meff_r c_r: the PGS scalar chain multiplies it by dl
             }
         }
     }
@@ -1461,15 +1462,17 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         // Common case (the block's rows all in its LDS pool).  Gauss-Seidel over the flattened (iteration,
         // row) sequence, restated for latency: with n_k the velocity before row k and dl_k its impulse change,
         //     J_k . n_k = J_k . n_(k-1) + dl_(k-1) c_k,    c_k = J_k . M^-1 J_(k-1)^T (precomputed per row),
-        // so the 16-lane reduction of J_k . n_(k-1) runs while row k-1 is solved, and the row-to-row
-        // dependency chain is 5 scalar ops (fma, sub, fma, med3, sub).  Row k+3 is read while row k is solved
+        // so the 16-lane reduction of J_k . n_(k-1) runs while row k-1 is solved, and the row update
+        //     lambda_k + meff_k (b_k - J_k . n_k) = P_k - q_k dl_(k-1),   P_k = lambda_k + meff_k (b_k - J_k . n_(k-1)),
+        // with q_k = meff_k c_k stored per row and P_k formed as soon as the reduction lands: the row-to-row
+        // dependency chain is 3 scalar ops (fma, med3, sub).  Row k+3 is read while row k is solved
         // (through a link stored in row k), two stages before its reduction needs it; the lambdas it reads were
         // stored earlier (LDS ops of a wave are ordered: the pool layout keeps a friction row >= 4 positions
         // after its normal row and a cycle >= 4 positions long, see pool_gap).
         // Branch-free bounds: lo = 0 for every row, normal and limit rows have mu = 0, friction rows hi = 0,
         // so [-mu ln, hi + mu ln] is exact for all.
         using T2 = typename std::conditional<sizeof(T) == 4, float2, double2>::type;
-        struct RowRegs { T j0, m0, j1, m1, b, hi, lam, meff, mu, c; int next3, next3_ln; };
+        struct RowRegs { T j0, m0, j1, m1, b, hi, lam, meff, mu, q; int next3, next3_ln; };
         const char* lds0 = reinterpret_cast<const char*>(shb);
         const int off0 = 2 * l * (int)sizeof(T), off1 = (l < NV - GL ? 2 * (GL + l) : RO_Z) * (int)sizeof(T);
         auto as_int = [](T v) -> int {
@@ -1484,11 +1487,11 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 const float4 s0 = *reinterpret_cast<const float4*>(R + RO_S0 * sizeof(T));
                 const float4 s1 = *reinterpret_cast<const float4*>(R + RO_S1 * sizeof(T));
                 d.b = s0.x; d.hi = s0.y; d.lam = s0.z; d.meff = s0.w;
-                d.mu = s1.x; d.c = s1.y; d.next3 = __float_as_int(s1.z); d.next3_ln = __float_as_int(s1.w);
+                d.mu = s1.x; d.q = s1.y; d.next3 = __float_as_int(s1.z); d.next3_ln = __float_as_int(s1.w);
             } else {
                 const T* S0 = reinterpret_cast<const T*>(R) + RO_S0;
                 d.b = S0[0]; d.hi = S0[1]; d.lam = S0[2]; d.meff = S0[3];
-                d.mu = S0[4]; d.c = S0[5]; d.next3 = as_int(S0[6]); d.next3_ln = as_int(S0[7]);
+                d.mu = S0[4]; d.q = S0[5]; d.next3 = as_int(S0[6]); d.next3_ln = as_int(S0[7]);
             }
         };
         auto load_ln = [&](int ln_off) -> T { return *reinterpret_cast<const T*>(lds0 + ln_off); };
@@ -1539,17 +1542,18 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             load(oC, C);
             // positions 0..2 are never friction rows (mu = 0): their bounds need no lambda
             T lnA = T(0), lnB = T(0), lnC = T(0), lnD;
-            T sA = row_sum(A.j0 * n0 + A.j1 * n1), sB, sC, sD, dlp = T(0);
+            // P of the row being solved, from its reduction one stage earlier (the first row's here)
+            T pA = fma(A.meff, A.b - row_sum(A.j0 * n0 + A.j1 * n1), A.lam), pB, pC, pD, dlp = T(0);
             // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read
-            auto stage = [&](auto masked, int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T sX,
-                             T& sY, T lnX, T& lnW) {
+            auto stage = [&](auto masked, int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T pX,
+                             T& pY, T lnX, T& lnW) {
                 oW = X.next3;
                 load(oW, W);
                 lnW = load_ln(X.next3_ln);
-                sY = row_sum(Y.j0 * n0 + Y.j1 * n1);
-                const T jv = sX + dlp * X.c;
+                pY = fma(Y.meff, Y.b - row_sum(Y.j0 * n0 + Y.j1 * n1), Y.lam);
                 const T lo = -(X.mu * lnX), hi = X.hi + X.mu * lnX;
-                const T lsol = med3(X.lam + X.meff * (X.b - jv), lo, hi);   // == clamp: lo <= hi always
+                const T tX = fma(-X.q, dlp, pX);
+                const T lsol = med3(tX, lo, hi);   // == clamp: lo <= hi always
                 T lnew = lsol;
                 if constexpr (decltype(masked)::value) lnew = kk < total ? lsol : X.lam;
                 *reinterpret_cast<T*>(const_cast<char*>(lds0) + oX + RO_LAM * sizeof(T)) = lnew;
@@ -1562,10 +1566,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 dlp = dl;
             };
             auto round = [&](auto masked, int k) {
-                stage(masked, k, A, B, D, oA, oD, sA, sB, lnA, lnD);
-                stage(masked, k + 1, B, C, A, oB, oA, sB, sC, lnB, lnA);
-                stage(masked, k + 2, C, D, B, oC, oB, sC, sD, lnC, lnB);
-                stage(masked, k + 3, D, A, C, oD, oC, sD, sA, lnD, lnC);
+                stage(masked, k, A, B, D, oA, oD, pA, pB, lnA, lnD);
+                stage(masked, k + 1, B, C, A, oB, oA, pB, pC, lnB, lnA);
+                stage(masked, k + 2, C, D, B, oC, oB, pC, pD, lnC, lnB);
+                stage(masked, k + 3, D, A, C, oD, oC, pD, pA, lnD, lnC);
             };
             int k = 0;
             for (; k < tmin; k += 4) round(std::false_type{}, k);
