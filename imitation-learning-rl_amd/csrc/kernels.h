@@ -82,7 +82,9 @@ __device__ inline double alive_reward(bool np1, float obs0) {
 }
 
 // ----------------------------------------------------------------------------------- SoA lane I/O
-__device__ inline void load_book(const KArgs& a, int i, Book& b) {
+// full = false: the cooperative kernel's low-level step, which overwrites robot_pos and the reward terms (dj, dvj,
+// bps, es, jls, alive, dlts) before it reads them (low_level_env.py:481-511): those 80 B are not fetched
+__device__ inline void load_book(const KArgs& a, int i, Book& b, bool full = true) {
     const int* bi = a.bi;
     b.frame = bi[0 * a.n + i]; b.timestep = bi[1 * a.n + i]; b.pred_idx = bi[2 * a.n + i];
     b.clip = bi[3 * a.n + i]; b.rng_ctr = (unsigned)bi[4 * a.n + i]; b.mode = (unsigned)bi[5 * a.n + i];
@@ -91,9 +93,12 @@ __device__ inline void load_book(const KArgs& a, int i, Book& b) {
         ? ((unsigned long long)(unsigned)bi[11 * a.n + i] | ((unsigned long long)(unsigned)bi[12 * a.n + i] << 32)) : 0ull;
     const double* d = a.bd;
     auto D = [&](int e) { return d[(long)e * a.n + i]; };
-    for (int k = 0; k < 3; k++) { b.target[k] = D(k); b.srp[k] = D(3 + k); b.robot_pos[k] = D(6 + k); b.sep[k] = D(9 + k); }
+    for (int k = 0; k < 3; k++) { b.target[k] = D(k); b.srp[k] = D(3 + k); b.sep[k] = D(9 + k); }
     b.hldt = D(12); b.wt[0] = D(13); b.wt[1] = D(14); b.lts = D(15);
-    b.dj = D(16); b.dvj = D(17); b.bps = D(18); b.es = D(19); b.jls = D(20); b.alive = D(21); b.dlts = D(22);
+    if (full) {
+        for (int k = 0; k < 3; k++) b.robot_pos[k] = D(6 + k);
+        b.dj = D(16); b.dvj = D(17); b.bps = D(18); b.es = D(19); b.jls = D(20); b.alive = D(21); b.dlts = D(22);
+    }
     if (a.hier) {
         b.level_rem = bi[8 * a.n + i]; b.n_high = bi[9 * a.n + i]; b.expect_high = bi[10 * a.n + i];
         b.hts = D(23); b.cum_drift = D(24); b.drift = D(25); b.dhts = D(26); b.cum_alive = D(27);
@@ -233,8 +238,9 @@ __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i,
 template <typename T>
 __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, long io, T* st, Book& b, const float* act,
                                                           unsigned& ef, const T* scs = nullptr,
-                                                          bool* defer_reset = nullptr) {   // defer_reset: the caller
-                                                                                           // runs the auto-reset and the store
+                                                          bool* defer_reset = nullptr,   // the caller runs the
+                                                                                         // auto-reset and the store
+                                                          float* obs_dst = nullptr) {    // obs row (default: a.obs)
     // i: the lane (state, bookkeeping); io: its output row of this step (t * n + i, hum_step_k)
     const ClipDev& c = a.clips[b.clip];
     float obs[HUM_NOBS];
@@ -306,8 +312,9 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         b.timestep += 1;
         if (b.timestep >= 3000) done = true;
     }
+    float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
 #pragma unroll
-    for (int k = 0; k < HUM_NOBS; k++) a.obs[io * HUM_NOBS + k] = obs[k];
+    for (int k = 0; k < HUM_NOBS; k++) orow[k] = obs[k];
     a.rew[io] = (float)total;
     a.done[io] = done ? 1 : 0;
     if (a.frame_out) a.frame_out[io] = b.frame;
@@ -434,7 +441,7 @@ __device__ inline float hier_update_reward_high(Book& b) {
 // physics of a low step; stores state/book and writes the dict-shaped outputs.
 template <typename T>
 __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, long io, T* st, Book& b, bool high, unsigned& ef,
-                                                          const T* scs = nullptr) {
+                                                          const T* scs = nullptr, bool store_state = true) {
     const ClipDev& c = a.clips[b.clip];
     b.robot_pos[0] = b.bxy[0]; b.robot_pos[1] = b.bxy[1]; b.robot_pos[2] = 0;   // step(): :358-361
     float obs[HUM_NOBS], js[NDOF], o44[HUM_NOBS_HIGH];
@@ -569,14 +576,16 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
             for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high_reset[io * HUM_NOBS_HIGH + k] = r44[k];
         }
     }
-    store_lane(a, i, st, b);
+    if (store_state) store_lane(a, i, st, b);
+    else store_book(a, i, b);
     if (ef) atomicOr(a.eflags, ef);
 }
 
 // non-finite action on a lane (humanoid.py:55 assert): lane not stepped, flagged, outputs neutral
-__device__ inline void nonfinite_outputs(const KArgs& a, long io, int frame) {
+__device__ inline void nonfinite_outputs(const KArgs& a, long io, int frame, float* obs_dst = nullptr) {
     if (!a.hier) {
-        for (int k = 0; k < HUM_NOBS; k++) a.obs[io * HUM_NOBS + k] = 0.f;
+        float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
+        for (int k = 0; k < HUM_NOBS; k++) orow[k] = 0.f;
     } else {
         a.rew_high[io] = 0.f;
         a.agents[io] = 0;
@@ -708,7 +717,9 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     const bool skip = a.hier && valid && a.agent_sel && sel == HUM_AGENT_SEL_SKIP;   // no action: lane untouched
     const bool high = a.hier && valid && !skip && (a.agent_sel ? sel != 0 : carry[0] != 0);
     const bool env_ok = high || ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
-    const bool any_phys = __ballot(valid && !high && !skip) != 0;   // wave-uniform
+    // an env that takes no physics step this round rides along with the wave's physics and keeps its LDS state
+    const bool frozen = !valid || skip || high || !env_ok;
+    const bool any_phys = __ballot(!frozen) != 0;   // wave-uniform
     // the env's terrain (HUM_TERRAIN_RANDOM_BLOCKS: drawn at its last reset)
     const unsigned long long tkey = TERRAIN && a.P.terrain == HUM_TERRAIN_RANDOM_BLOCKS && valid
         ? ((unsigned long long)(unsigned)carry[1] | ((unsigned long long)(unsigned)carry[2] << 32)) : 0ull;
@@ -717,7 +728,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
 #pragma unroll 1
         for (int s = 0; s < a.P.nsub; s++)
             group_substep<T, EPB_, TERRAIN>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_block_size(EPB_, a.P.lds_rows),
-                                   l, ef, tkey);
+                                   l, ef, tkey, frozen);
     }
     // hinge sin / cos of the final physics state, one dof per lane, for calc_state's kinematics on lane 0
     T* scs = &sh[ge].x.aba.IA[0][0];
@@ -727,42 +738,47 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         scs[2 * d] = sn;
         scs[2 * d + 1] = cs;
     }
+    // LDS staging of the low-level env's output rows (the ABA scratch is dead after the physics): lane 0 writes
+    // them, then every lane of the env stores its share, 16 consecutive words per store instruction
+    // (IA words [0, 70): the hinge sin / cos below and the reset exchange; [72, 142): obs; [144, 214): reset obs)
+    float* ostage = reinterpret_cast<float*>(scs + 72);    // this step's observation
+    float* rstage = reinterpret_cast<float*>(scs + 144);   // the auto-reset observation
+    static_assert(sizeof(sh[0].x.aba.IA) >= (144 + HUM_NOBS) * sizeof(T) && 2 * NDOF + 2 + 2 * NDOF <= 72,
+                  "output row staging");
     wave_sync();
     PHASE_INIT;
     Book b;
     T st[HUM_NSTATE];
-    bool rst = false, stored = false;
+    bool rst = false, booked = false;
     if (valid && l == 0 && skip) {
         a.agents[io] = 0;
     } else if (valid && l == 0) {
-        load_book(a, i, b);
+        load_book(a, i, b, a.hier != 0);
         SUBPHASE(17);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
-            nonfinite_outputs(a, io, b.frame);
+            nonfinite_outputs(a, io, b.frame, a.hier ? nullptr : ostage);
         } else {
-            if (high) {   // physics (if the wave ran it) is discarded: the HBM state is the current one
+            // the env's current state (a frozen env's: unchanged by the wave's physics)
 #pragma unroll
-                for (int e = 0; e < HUM_NSTATE; e++) st[e] = ((const T*)a.phys)[(long)e * a.n + i];
-            } else {
-#pragma unroll
-                for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
-            }
+            for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
+            booked = true;
             if (a.hier) {
-                hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs);   // high: the HBM state, not S.st
-                stored = true;
+                hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs, false);
+#pragma unroll
+                for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];   // an auto-reset replaced it
             } else {
                 float act[HUM_NACT];
 #pragma unroll
                 for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[io * HUM_NACT + k];
-                post_step(a, i, io, st, b, act, ef, scs, &rst);
+                post_step(a, i, io, st, b, act, ef, scs, &rst, ostage);
             }
         }
     }
     SUBPHASE(18);
     if (!a.hier) {
         // auto-reset (low-level env): lane 0 draws the start frame (reset_lane's first draw), the env's lanes
-        // compute the reset pose's hinge sin / cos, lane 0 finishes reset_lane with them and stores the lane
+        // compute the reset pose's hinge sin / cos, lane 0 finishes reset_lane with them
         int* xch = reinterpret_cast<int*>(scs + 2 * NDOF);
         if (valid && l == 0) {
             int sf = -1;
@@ -789,36 +805,42 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             }
             wave_sync();
         }
-        if (valid && l == 0 && env_ok) {
+        if (valid && l == 0 && booked) {
             if (rst) {
                 float o2[HUM_NOBS];
                 reset_lane(a, i, st, b, sf, 0.0, o2, ef, scs_r);
-                if (a.obs_reset) {
 #pragma unroll
-                    for (int k = 0; k < HUM_NOBS; k++) a.obs_reset[io * HUM_NOBS + k] = o2[k];
-                }
+                for (int k = 0; k < HUM_NOBS; k++) rstage[k] = o2[k];
+#pragma unroll
+                for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];
             }
-            store_lane(a, i, st, b);
-            stored = true;
+            store_book(a, i, b);
+        }
+        wave_sync();
+        if (valid) {   // the output rows, coalesced
+            float* orow = a.obs + io * HUM_NOBS;
+            for (int k = l; k < HUM_NOBS; k += GL) orow[k] = ostage[k];
+            if (sf >= 0 && a.obs_reset) {
+                float* rrow = a.obs_reset + io * HUM_NOBS;
+                for (int k = l; k < HUM_NOBS; k += GL) rrow[k] = rstage[k];
+            }
         }
     }
     PHASE(10);
-    if (a.ksteps > 1) {   // wave-uniform: publish the env's state for the next step of this launch
-        if (valid && l == 0) {
-            if (!stored) {   // not stepped (no action / non-finite action): the stored state stands
-#pragma unroll
-                for (int e = 0; e < HUM_NSTATE; e++) st[e] = ((const T*)a.phys)[(long)e * a.n + i];
-            } else {
-                carry[0] = b.expect_high;
-                carry[1] = (int)(unsigned)(b.terrain_key & 0xffffffffull);
-                carry[2] = (int)(unsigned)(b.terrain_key >> 32);
-            }
-#pragma unroll
-            for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];
-        }
-        __syncthreads();
+    if (valid && l == 0 && booked) {   // the per-env integers the next step's lanes read
+        carry[0] = a.hier ? b.expect_high : 0;
+        carry[1] = (int)(unsigned)(b.terrain_key & 0xffffffffull);
+        carry[2] = (int)(unsigned)(b.terrain_key >> 32);
     }
+    __syncthreads();
     }   // steps of the launch
+    {   // the launch's final physics state (it stays in LDS between the steps): each lane of an env stores its share
+        const int l = threadIdx.x & (GL - 1), ge = threadIdx.x / GL, i = blk * EPB_ + ge;
+        if (i < a0.n) {
+#pragma unroll
+            for (int e = l; e < HUM_NSTATE; e += GL) ((T*)a0.phys)[(long)e * a0.n + i] = sh[ge].st[e];
+        }
+    }
 #ifdef HUM_WLOG_ON
     if (threadIdx.x == 0) {   // wave duration: max (tail) and mean
         const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t_wave0;

@@ -1033,7 +1033,8 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
 template <typename T, int EPB_, bool TERRAIN = false>   // TERRAIN: heightfield ground (hum_set_terrain)
 __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>* shb, const int ge,
                                                              T* gblock, const int l, unsigned& ef,
-                                                             unsigned long long tkey) {   // tkey: terrain 2
+                                                             unsigned long long tkey,   // tkey: terrain 2
+                                                             const bool frozen = false) {   // env takes no step
     GroupLDS<T>& S = shb[ge];
     const ModelTab<T>& M = tab_fresh<T>();
     const T dt = (T)P.dt;
@@ -1605,8 +1606,9 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     PHASE(8);
     S.nu[l] = n0;
     if (l < NV - GL) S.nu[GL + l] = n1;
-    // ---- integrate (lanes split the state), lane 0 the quaternion
-    {
+    // ---- integrate (lanes split the state), lane 0 the quaternion.  A frozen env (no action this round, a
+    //      non-finite action, or the hierarchical env's high-level turn) rides along with the wave and keeps its state.
+    if (!frozen) {
         if (l < 3) { S.st[10 + l] = S.nu[l]; S.st[7 + l] = S.nu[3 + l]; S.st[l] += dt * S.nu[3 + l]; }
         for (int j = l; j < NDOF; j += GL) { S.st[30 + j] = S.nu[6 + j]; S.st[13 + j] += dt * S.nu[6 + j]; }
         if (l == 0) {

@@ -19,6 +19,7 @@ HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
 HUM_RESET_NO_REF_POSE, HUM_RESET_NO_INIT_VEL = 1, 2
 HUM_MAX_CONTACTS = 95
 HUM_TERRAIN_PLANE, HUM_TERRAIN_HEIGHTFIELD, HUM_TERRAIN_RANDOM_BLOCKS = 0, 1, 2
+HUM_OK, HUM_ERR_ARG, HUM_ERR_HIP, HUM_ERR_NOCLIP, HUM_ERR_STATE = 0, -1, -2, -3, -4
 
 # bookkeeping layout (HUM_BK_*)
 BK = dict(frame=0, cur_timestep=1, rng_counter=2, predefinedTargetIndex=3, target=4, starting_robot_pos=7,

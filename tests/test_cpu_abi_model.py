@@ -29,6 +29,19 @@ def test_library_exports_every_header_symbol():
     assert L.hum_abi_version() == N.HUM_ABI_VERSION
 
 
+def test_python_constants_match_header():
+    """Every integer HUM_* constant of the ctypes mirror equals the header's #define of the same name, and every
+    #define the mirror could need (status codes, step / reset / mode / flag bits) is present in it."""
+    defs = dict(re.findall(r"^#define\s+(HUM_\w+)\s+(-?\d+)u?\b", open(HEADER).read(), re.M))
+    mirror = {k: v for k, v in vars(N).items() if k.startswith("HUM_") and isinstance(v, int)}
+    for k, v in mirror.items():
+        if k in defs:
+            assert v == int(defs[k]), k
+    for k in defs:
+        if k.startswith(("HUM_OK", "HUM_ERR_", "HUM_STEP_", "HUM_RESET_", "HUM_MODE_", "HUM_EFLAG_", "HUM_AGENT_")):
+            assert k in mirror, k
+
+
 def test_config_layout_matches_header(tmp_path):
     """Compile a tiny C program against the header and compare sizeof/offsetof with ctypes."""
     src = tmp_path / "layout.c"

@@ -244,8 +244,10 @@ def test_hier_physics_fp32_matches_oracle(golden_hier, name):
     """The benchmarked fp32 kernel with full physics on the golden two-level scenarios vs the fp64 oracle physics
     (one call each from the recorded state): the fp32 step bound of the configs 2 / 3 / 5 scale tests on every
     well-conditioned low-level call (oracle obs moving by <= 1e-5 under a 2^-24 relative input perturbation),
-    agents / done / frame / counters exact there."""
-    from test_gpu_scale import FP32_BOUND, SENS_BOUND
+    agents / done / frame / counters exact there.  Ill-conditioned calls (at most MAX_ILL_FRACTION of the low-level
+    calls, or one in a short scenario) are checked instead through the fp64 kernel from the identical state: the
+    exclusion is the model's discontinuity, not the kernel's."""
+    from test_gpu_scale import FP32_BOUND, FP64_BOUND, MAX_ILL_FRACTION, SENS_BOUND
     r = rec(golden_hier, name)
     o = run_scenario(r, "fp32", skip_physics=False, kernel=1)
     hl = r["has_low"].astype(bool)
@@ -258,7 +260,13 @@ def test_hier_physics_fp32_matches_oracle(golden_hier, name):
         ref = O.calc_state(O.phys_step(r["state_pre"][t], tau), wt)[0]
         pert = O.calc_state(O.phys_step(r["state_pre"][t] * (1 + 2.0 ** -24 * rng.choice([-1.0, 1.0], 47)), tau), wt)[0]
         good[t] = np.abs(pert - ref).max() <= SENS_BOUND
-    assert good.sum() >= 0.8 * len(good)
+    ill = ~good
+    assert ill.sum() <= max(1, int(MAX_ILL_FRACTION * low_call.sum()))
+    if ill.any():
+        o64 = run_scenario(r, "fp64", skip_physics=False, kernel=1)
+        m64 = ill & hl
+        assert np.abs(o64["ol"][m64] - r["obs_low"][m64]).max(initial=0) <= FP64_BOUND["obs_max"]
+        np.testing.assert_array_equal(o64["done"][ill], r["done"][ill])
     np.testing.assert_array_equal(o["done"][good], r["done"][good])
     np.testing.assert_array_equal(o["frame"][good], r["book_selected_motion_frame"][good].astype(np.int32))
     m = hl & good

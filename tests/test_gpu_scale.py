@@ -52,6 +52,17 @@ MAX_ILL_FRACTION = 0.2
 FP64_BOUND = {"obs_max": 1e-5, "reward_max": 1e-5, "state_max": 1e-6}
 
 
+def unit_quat(phys):
+    """The states with the base quaternion renormalised in float64.  An fp32 state's quaternion is unit only to
+    float32 rounding (|q|^2 - 1 ~ 1e-7), so its rotation matrix is orthogonal only to that; the kernel (world-frame
+    spatial algebra) and the oracle (local-frame, pybullet's link layout) use R^T as R^-1 in different places and
+    the dynamics amplify the 1e-7 difference by up to ~1e7 on stiff states (measured: fp64 kernel vs oracle 1.2e-4
+    from a raw fp32 state, 1e-12 from the same state renormalised).  The fp64 cross-check starts from these."""
+    p = np.array(phys, dtype=np.float64, copy=True)
+    p[..., 3:7] /= np.linalg.norm(p[..., 3:7], axis=-1, keepdims=True)
+    return p
+
+
 def _sample_lanes(book, c, name, per_clip, n):
     lanes = np.nonzero(book[:, BK["clip"]].astype(int) == c)[0]
     if name == "motion13_13":   # the reference raises IndexError past the 120-row velocity table
@@ -72,9 +83,12 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
     obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
     phys2, book2 = env.get_state()
     env.close()
-    # the fp64 kernel from the identical state (checks the lanes the fp32 bound excludes)
-    env64 = HumanoidVecEnv(n, clips=clips, seed=seed, precision="fp64")
-    env64.set_state(phys, book)
+    # the fp64 kernel from the identical state, base quaternion renormalised (checks the lanes the fp32 bound
+    # excludes; see unit_quat)
+    physn = unit_quat(phys)
+    env64 = HumanoidVecEnv(n, clips=clips, seed=seed, precision="fp64",
+                           kernel=int(os.environ.get("ILRL_FP64_CHECK_KERNEL", "1")))   # diagnostics: 0 = per-lane
+    env64.set_state(physn, book)
     obs64, rew64, done64, _ = [x.cpu().numpy() for x in env64.step(torch.as_tensor(a, device="cuda"))]
     phys64, _ = env64.get_state()
     env64.close()
@@ -90,10 +104,12 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
             st["rew"].append(abs(float(rew[i]) - rr))
             st["done"].append(bool(done[i]) != rd)
             st["state"].append(np.abs(phys2[i] - o.state).max())
-            st["obs64"].append(np.abs(obs64[i] - ro).max())
-            st["rew64"].append(abs(float(rew64[i]) - rr))
-            st["done64"].append(bool(done64[i]) != rd)
-            st["state64"].append(np.abs(phys64[i] - o.state).max())
+            o64 = oracle_from_lane(clip, physn[i], book[i])
+            ro64, rr64, rd64, _ = o64.step(a[i])
+            st["obs64"].append(np.abs(obs64[i] - ro64).max())
+            st["rew64"].append(abs(float(rew64[i]) - rr64))
+            st["done64"].append(bool(done64[i]) != rd64)
+            st["state64"].append(np.abs(phys64[i] - o64.state).max())
             p = oracle_from_lane(clip, phys[i] * (1 + 2.0 ** -24 * prng.choice([-1.0, 1.0], 47)), book[i])
             st["sens"].append(np.abs(p.step(a[i])[0] - ro).max())
             st["frame_ok"] &= int(frame[i]) == o.frame and int(book2[i, BK["cur_timestep"]]) == o.cur_timestep
@@ -206,9 +222,9 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
     T = lambda x: torch.as_tensor(x, device="cuda")
     outs = {}
     for prec, e in ((precision, env), ("fp64", None)):
-        if e is None:   # the fp64 kernel from the identical state
+        if e is None:   # the fp64 kernel from the identical state, base quaternion renormalised (unit_quat)
             e = HierVecEnv(n, seed=seed, precision="fp64")
-            e.set_state(phys, book)
+            e.set_state(unit_quat(phys), book)
         res = [x.cpu().numpy() for x in e.step(T(ah), T(al))]
         outs[prec if e is env else "f64"] = res + list(e.get_state())
         e.close()
@@ -233,7 +249,7 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
                          ("num_high_level_steps", o.num_high_level_steps)):
                 st["exact_ok"] &= int(book2[i, BK[k]]) == int(v)
 
-            def errs(obs_h, obs_l, r_h, r_l):
+            def errs(obs_h, obs_l, r_h, r_l, robs, rrew):
                 e = 0.0
                 if OH.HIGH in robs:
                     e = max(e, float(np.abs(obs_h[i] - robs[OH.HIGH]).max()))
@@ -241,16 +257,18 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
                     e = max(e, float(np.abs(obs_l[i] - robs[OH.LOW]).max()))
                 r = max(abs(float(r_h[i]) - float(rrew.get(OH.HIGH, 0))), abs(float(r_l[i]) - float(rrew.get(OH.LOW, 0))))
                 return e, r
-            eo, er = errs(oh, ol, rh, rl)
-            eo64, er64 = errs(oh64, ol64, rh64, rl64)
+            eo, er = errs(oh, ol, rh, rl, robs, rrew)
+            o64 = OH.OracleHierEnv.from_lane(clip, unit_quat(phys[i]), book[i], BK)   # the fp64 cross-check's
+            robs64, rrew64, rdone64, _ = o64.step(act)
+            eo64, er64 = errs(oh64, ol64, rh64, rl64, robs64, rrew64)
             st["obs"].append(eo)
             st["rew"].append(er)
             st["done"].append(bool(done[i]) != rdone["__all__"])
             st["state"].append(float(np.abs(phys2[i] - o.state).max()))
             st["obs64"].append(eo64)
             st["rew64"].append(er64)
-            st["done64"].append(bool(d64[i]) != rdone["__all__"])
-            st["state64"].append(float(np.abs(p64[i] - o.state).max()))
+            st["done64"].append(bool(d64[i]) != rdone64["__all__"])
+            st["state64"].append(float(np.abs(p64[i] - o64.state).max()))
             if kind:
                 st["sens"].append(0.0)   # no physics: no discontinuity
             else:
