@@ -118,6 +118,14 @@ __device__ inline void rot_post(T* M, int ax, T c, T s) {
     }
 }
 
+// acc + x * c for a model constant c, as the fma that fp-contraction forms for `acc + x * c`: a term with c == 0 is
+// skipped (fma(x, 0, acc) == acc up to the sign of a zero result) and c == 1 folds to an add, so the identity
+// rotations and zero offsets of the model cost nothing while every other term rounds exactly as before.
+template <typename T>
+__device__ __attribute__((always_inline)) inline T fmak(T x, double c, T acc) {
+    return c == 0.0 ? acc : fma(x, (T)c, acc);
+}
+
 template <typename T>
 __device__ inline void quat_to_mat(const T* q, T* R) {
 #pragma clang fp contract(on)   // per-expression fusion only: the same frames in every inlining context
@@ -175,13 +183,18 @@ __device__ inline void forward_kinematics_pre(const T* quat, const T* scs, Kin<T
 #pragma unroll
         for (int r = 0; r < 3; r++)
 #pragma unroll
-            for (int c = 0; c < 3; c++)
-                M[3 * r + c] = K.R[p][3 * r] * (T)body_Roff[9 * b + c] + K.R[p][3 * r + 1] * (T)body_Roff[9 * b + 3 + c] +
-                               K.R[p][3 * r + 2] * (T)body_Roff[9 * b + 6 + c];
+            for (int c = 0; c < 3; c++) {   // R_p Roff: (R0 c0 + R1 c1) + R2 c2, fused as written
+                const double c0 = body_Roff[9 * b + c];
+                T m = c0 == 0.0 ? T(-0.0) : K.R[p][3 * r] * (T)c0;
+                m = fmak(K.R[p][3 * r + 1], body_Roff[9 * b + 3 + c], m);
+                M[3 * r + c] = fmak(K.R[p][3 * r + 2], body_Roff[9 * b + 6 + c], m);
+            }
 #pragma unroll
-        for (int i = 0; i < 3; i++)
-            K.o[b][i] = K.o[p][i] + K.R[p][3 * i] * (T)body_toff[3 * b] + K.R[p][3 * i + 1] * (T)body_toff[3 * b + 1] +
-                        K.R[p][3 * i + 2] * (T)body_toff[3 * b + 2];
+        for (int i = 0; i < 3; i++) {
+            T o = fmak(K.R[p][3 * i], body_toff[3 * b], K.o[p][i]);
+            o = fmak(K.R[p][3 * i + 1], body_toff[3 * b + 1], o);
+            K.o[b][i] = fmak(K.R[p][3 * i + 2], body_toff[3 * b + 2], o);
+        }
 #pragma unroll
         for (int k = 0; k < body_ndof[b]; k++) {
             const int d = body_dof0[b] + k, ax = dof_axis[d];
@@ -917,9 +930,11 @@ __device__ inline void part_positions(const Kin<T>& K, T (*pp)[3]) {
         const int b = part_body[k];
         if (b < 0) { pp[k][0] = pp[k][1] = pp[k][2] = 0; continue; }
 #pragma unroll
-        for (int i = 0; i < 3; i++)
-            pp[k][i] = K.o[b][i] + K.R[b][3 * i] * (T)part_p[3 * k] + K.R[b][3 * i + 1] * (T)part_p[3 * k + 1] +
-                       K.R[b][3 * i + 2] * (T)part_p[3 * k + 2];
+        for (int i = 0; i < 3; i++) {
+            T v = fmak(K.R[b][3 * i], part_p[3 * k], K.o[b][i]);
+            v = fmak(K.R[b][3 * i + 1], part_p[3 * k + 1], v);
+            pp[k][i] = fmak(K.R[b][3 * i + 2], part_p[3 * k + 2], v);
+        }
     }
 }
 

@@ -296,6 +296,7 @@ __device__ inline void load_tab_lds() {   // block-wide; the caller's __syncthre
 #ifndef HUM_MAXR_LDS
 #define HUM_MAXR_LDS 30
 #endif
+
 constexpr int MAXR_LDS = HUM_MAXR_LDS;
 
 template <typename T>
@@ -1573,6 +1574,14 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 stage(masked, k + 3, D, A, C, oD, oC, pD, pA, lnD, lnC);
             };
             int k = 0;
+            // two rounds per iteration: the scheduler sinks a round's last row-ahead loads to the loop end, where the
+            // next iteration's first stage waits for them (lgkmcnt(0)); with 8 stages per iteration half as many
+            // loads cross the back edge (+0.5 %, profiles/r03_pgs_sched_ab.txt; pinning the loads with
+            // sched_barrier instead measured -0.5 %)
+            for (; k + 8 <= tmin; k += 8) {
+                round(std::false_type{}, k);
+                round(std::false_type{}, k + 4);
+            }
             for (; k < tmin; k += 4) round(std::false_type{}, k);
             for (; k < tmax; k += 4) round(std::true_type{}, k);
         }

@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 L=$PWD/imitation-learning-rl_amd/ilrl_amd/_lib
-for rep in ${REPS:-1}; do
+for rep in $(seq ${REPS:-1}); do
 for n in ${LIBS:-default}; do
   for k in ${KS:-1 8}; do
     lib=$L/libhumenv_$n.so; [ "$n" = default ] && lib=$L/libhumenv.so
