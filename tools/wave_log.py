@@ -8,22 +8,23 @@ import torch
 from ilrl_amd import _native as N
 from ilrl_amd.vec_env import HumanoidVecEnv
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 1   # env steps per launch (hum_step_k); per-step figures divide by K
 nb = n // 4
 env = HumanoidVecEnv(n, clips=("motion02_04",), seed=0)
 env.reset()
 L = N.lib()
 L.hum_debug_wave_log.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
 g = torch.Generator(device="cuda").manual_seed(1)
-pool = [(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1) for _ in range(8)]
+pool = [(torch.rand(K, n, 17, device="cuda", generator=g) * 2 - 1).contiguous() for _ in range(8)]
 for s in range(10):
-    env.step(pool[s % 8], autoreset=True)
+    env.step_k(pool[s % 8], autoreset=True)
 rows = []
 buf = np.zeros((nb, 32), np.uint32)
 for s in range(30):
     L.hum_debug_wave_log(None, nb, 1)
-    _, _, done, _ = env.step(pool[s % 8], autoreset=True)
+    _, _, done, _ = env.step_k(pool[s % 8], autoreset=True)[:4]
     L.hum_debug_wave_log(buf.ctypes.data, nb, 0)
-    d = done.cpu().numpy().reshape(nb, 4).sum(1)
+    d = done.cpu().numpy().reshape(K, nb, 4).sum((0, 2))
     rows.append(np.column_stack([buf[:, :5].astype(np.float64), d, np.full(nb, s), buf[:, 9:32].astype(np.float64)]))
     st = buf[:, 5].astype(np.int64)
     st = (st - st.min()) % (1 << 32)
@@ -51,6 +52,9 @@ for s in range(30):
         simd = (hw >> 4) & 3
         print("   xcc histogram %s; simd histogram %s" % (np.bincount(xcc).tolist(), np.bincount(simd).tolist()))
 X = np.concatenate(rows)
+print("env steps per launch K = %d (per-block-step figures below are per env step: launch totals / K)" % K)
+X[:, [0, 1, 2, 3, 4, 5]] /= K
+X[:, 7:30] /= K
 dur = X[:, 0]
 names = ["pgs_len(sum max nrows)", "row_rounds", "narrow_rounds", "resets"]
 feat = X[:, [1, 2, 3, 5]]
