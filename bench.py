@@ -31,7 +31,7 @@ BYTES_PER_STEP_LAYOUT = 2 * 47 * 4 + 2 * (23 * 8 + 8 * 4) + 17 * 4 + 70 * 4 + 4 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3       # MI355X FP32 vector (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector
-K_DEFAULT = 8                  # env steps per launch (hum_step_k), DESIGN.md section 5
+K_DEFAULT = 32                 # env steps per launch (hum_step_k), DESIGN.md section 5 (k sweep)
 
 
 def parse():
@@ -182,19 +182,25 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     k = k or a.k
     if a.policy:
         k = 1   # closed loop: the policy acts on every step's observation
-    launches, wlaunches = -(-steps // k), -(-warmup // k)
+    # launch sizes: whole launches of k env steps, then one shorter launch for the remainder, so exactly `steps`
+    # (and `warmup`) env steps run
+    sizes = [k] * (steps // k) + ([steps % k] if steps % k else [])
+    wsizes = [k] * (warmup // k) + ([warmup % k] if warmup % k else [])
+    launches, wlaunches = len(sizes), len(wsizes)
     pool, hpool = _pools(a, dev, n, k, rank)
     G = a.gather_every
-    if G and G % k:
-        raise SystemExit("--gather-every must be a multiple of --k")
+    if G and (G % k or steps % k):
+        raise SystemExit("--gather-every: it and --steps must be multiples of --k")
     ring = [None] * (G // k if G else 1)   # output buffers of the launches since the last gather
     if a.hier:
         from ilrl_amd.hier_env import HierVecEnv
         env = HierVecEnv(n, seed=0, device=dev.index, lane_offset=rank * n, precision=precision, block_size=a.block,
                          **phys)
 
-        def step(s):
+        def step(s, kk=k):
             j = s % len(ring)
+            if kk < k:   # the remainder launch
+                return env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True)
             ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
     else:
         from ilrl_amd.clips import CLIP_NAMES
@@ -203,21 +209,23 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         env = HumanoidVecEnv(n, clips=clips, seed=0, device=dev.index, lane_offset=rank * n, precision=precision,
                              block_size=a.block, **phys)
 
-        def step(s):
+        def step(s, kk=k):
             j = s % len(ring)
+            if kk < k:   # the remainder launch
+                return env.step_k(pool[s % 16][:kk], autoreset=True)
             ring[j] = env.step_k(pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:
             from ilrl_amd.policy import DevicePolicy
             pol = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
             actbuf = torch.zeros(n, 17, device=dev)
 
-            def step(s):
+            def step(s, kk=1):
                 pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s, out=actbuf)
                 return env.step(actbuf, autoreset=True)
     env.reset()
     env.done.zero_()
     for w in range(wlaunches):
-        step(w)
+        step(w, wsizes[w])
     gather_s, gathered = 0.0, []
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -228,7 +236,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     t0 = time.perf_counter()
     ev0.record(stream)
     for s in range(launches):
-        step(s)
+        step(s, sizes[s])
         if G and world > 1 and not a.policy and ((s + 1) * k) % G == 0:
             tg = time.perf_counter()
             frag = _fragment(a, ring, [pool[(s - j) % 16] for j in range(len(ring) - 1, -1, -1)])
@@ -243,11 +251,11 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / (launches * k)   # per env step, on the launch stream (torch's current)
+    kern_ms = ev0.elapsed_time(ev1) / steps   # per env step, on the launch stream (torch's current)
     wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if world > 1 else wall
     low_steps = None
     if a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
-        low_steps = float(count_hier_low_steps(a, dev, n, precision, launches, wlaunches, k, phys, rank))
+        low_steps = float(count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank))
         if world > 1:
             low_steps = _all_reduce(world, dev, a.backend, low_steps, dist.ReduceOp.SUM)   # all ranks
     return env, wall, kern_ms, low_steps, gather_s, gathered
@@ -272,7 +280,7 @@ def _fragment(a, ring, acts):
     return [cat([r[0] for r in ring]), cat(acts), cat([r[1] for r in ring]), cat([r[2] for r in ring])]
 
 
-def count_hier_low_steps(a, dev, n, precision, launches, wlaunches, k, phys, rank):
+def count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank):
     """Lanes that take a low-level (physics) step in each transition of the timed launches: a lane acts high next
     iff its last outputs carried the high-level obs (level hand-back, or done -> auto-reset)."""
     import torch
@@ -282,12 +290,14 @@ def count_hier_low_steps(a, dev, n, precision, launches, wlaunches, k, phys, ran
     env = HierVecEnv(n, seed=0, device=dev.index, lane_offset=rank * n, precision=precision, block_size=a.block, **phys)
     env.reset()
     expect_high = torch.ones(n, dtype=torch.bool, device=dev)
-    low, out = 0, None
-    for s in range(wlaunches + launches):
-        out = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=out)
+    low = 0
+    # the same launches as run(): warm-up launch w reads pool block w % 16, timed launch s block s % 16
+    seq = [(w, kk, False) for w, kk in enumerate(wsizes)] + [(s, kk, True) for s, kk in enumerate(sizes)]
+    for s, kk, timed in seq:
+        out = env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True)
         agents, done = out[0], out[5]
-        for t in range(k):
-            if s >= wlaunches:
+        for t in range(kk):
+            if timed:
                 low += int((~expect_high).sum().item())
             expect_high = ((agents[t] & N.HUM_AGENT_HIGH) != 0) | (done[t] != 0)
     env.close()
@@ -321,8 +331,6 @@ def main():
         a.k = 1
     if a.k < 1:
         raise SystemExit("--k must be >= 1")
-    a.steps = -(-a.steps // a.k) * a.k      # whole launches
-    a.warmup = -(-a.warmup // a.k) * a.k
     env, wall_max, kern_ms, low_steps, gather_s, gathered = run(a, world, rank, dev, n, a.precision, a.steps, a.warmup,
                                                                 phys)
     flags = env.error_flags()
