@@ -32,9 +32,16 @@ constexpr double REWARD_W[7] = {0.34, 0.1, 0.34, 0.034, 0.15, 0.034, 0.1};   // 
 constexpr int EP_RIGHT_LEG = 6, EP_RIGHT_FOOT = 9;
 constexpr int PART_RIGHT_FOOT = 12;   // index of 'right_foot' in the pybullet parts order
 
+#define HUM_GLOBAL __attribute__((address_space(1)))
 struct ClipDev {
     const double* pos; const double* vel; const double* rel; const double* ep;
     int n_pos, n_vel, n_rel, n_ep, max_frame;
+    // the tables as global-address-space pointers: loaded from a device struct, the plain pointers are generic, and
+    // generic (flat) loads also count against the LDS counter, so every LDS wait nearby waited for the table fetches
+    __device__ const HUM_GLOBAL double* gpos() const { return (const HUM_GLOBAL double*)pos; }
+    __device__ const HUM_GLOBAL double* gvel() const { return (const HUM_GLOBAL double*)vel; }
+    __device__ const HUM_GLOBAL double* grel() const { return (const HUM_GLOBAL double*)rel; }
+    __device__ const HUM_GLOBAL double* gep() const { return (const HUM_GLOBAL double*)ep; }
 };
 
 struct Book {   // per-lane bookkeeping (mirrors HUM_BK_* in include/humanoid_env.h)
@@ -176,8 +183,8 @@ __device__ inline void ref_obs(const ClipDev& c, int frame, float* out28, unsign
     if (vrow >= c.n_vel) { vrow = c.n_vel - 1; eflags |= 2u; }   // HUM_EFLAG_VEL_ROW (motion13_13)
 #pragma unroll
     for (int j = 0; j < NREF; j++) {
-        out28[2 * j] = (float)c.rel[frame * 14 + JM_COL[j]];
-        out28[2 * j + 1] = (float)c.vel[vrow * 14 + JM_COL[j]];
+        out28[2 * j] = (float)c.grel()[frame * 14 + JM_COL[j]];
+        out28[2 * j + 1] = (float)c.gvel()[vrow * 14 + JM_COL[j]];
     }
 }
 

@@ -191,8 +191,8 @@ __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i,
         if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
 #pragma unroll
         for (int j = 0; j < NREF; j++) {
-            st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
-            st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+            st[13 + JM_DOF[j]] = (T)c.gpos()[start_frame * 14 + JM_COL[j]];
+            st[30 + JM_DOF[j]] = (T)c.gvel()[vrow * 14 + JM_COL[j]];
         }
     }
     for (int k = 0; k < 3; k++) { b.robot_pos[k] = 0; b.srp[k] = 0; }      // :264-268
@@ -209,8 +209,8 @@ __device__ __attribute__((always_inline)) void reset_lane(const KArgs& a, int i,
     const double phi = degToTarget * DEG2RAD;
     const double qz = sin(phi / 2), qw = cos(phi / 2);
     const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
-    const double* e0 = c.ep + f0 * 27;
-    const double* e1 = c.ep + f1 * 27;
+    const HUM_GLOBAL double* e0 = c.gep() + f0 * 27;
+    const HUM_GLOBAL double* e1 = c.gep() + f1 * 27;
     {
         const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
         const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
@@ -249,18 +249,19 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
     int jal;
     PostPhys<T> pp;
     calc_state(st, b.wt, obs, js, jal, pp, scs);
+    SUBPHASE(19);
     b.robot_pos[0] = pp.bx; b.robot_pos[1] = pp.by; b.robot_pos[2] = 0;
     // updateReward (:441-465)
     double dJ = 0, dV = 0;
 #pragma unroll
     for (int j = 0; j < NREF; j++) {
-        dJ = dJ + fabs(pp.q[JM_DOF[j]] - c.pos[b.frame * 14 + JM_COL[j]]) * JM_W[j];
+        dJ = dJ + fabs(pp.q[JM_DOF[j]] - c.gpos()[b.frame * 14 + JM_COL[j]]) * JM_W[j];
     }
     int vrow = b.frame;
     if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
 #pragma unroll
     for (int j = 0; j < NREF; j++) {
-        dV = dV + fabs(pp.qd[JM_DOF[j]] - c.vel[vrow * 14 + JM_COL[j]]) * JM_WV[j];
+        dV = dV + fabs(pp.qd[JM_DOF[j]] - c.gvel()[vrow * 14 + JM_COL[j]]) * JM_WV[j];
     }
     const double jointScore = exp(4 * (-dJ / JOINT_WEIGHT_SUM));
     const double jointVelScore = exp((-dV / JOINT_VEL_WEIGHT_SUM) / 2);
@@ -287,6 +288,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
     total = total + b.alive * REWARD_W[5];
     total = total + b.bps * REWARD_W[6];
     inc_frame(b, c, 2);                                                      // :513
+    SUBPHASE(20);
     // checkTarget (:412-434)
     {
         const double dist = norm3_blas(b.robot_pos[0] - b.target[0], b.robot_pos[1] - b.target[1], b.robot_pos[2] - b.target[2]);
@@ -302,6 +304,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         }
         set_walk_target_hl(b);
     }
+    SUBPHASE(21);
     ref_obs(c, b.frame, obs + 42, ef);                                        // :519
     bool done;                                                                // :521-524
     {
@@ -312,6 +315,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         b.timestep += 1;
         if (b.timestep >= 3000) done = true;
     }
+    SUBPHASE(22);
     float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
 #pragma unroll
     for (int k = 0; k < HUM_NOBS; k++) orow[k] = obs[k];
@@ -386,8 +390,8 @@ __device__ __attribute__((always_inline)) void hier_reset_lane(const KArgs& a, i
         if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
 #pragma unroll
         for (int j = 0; j < NREF; j++) {
-            st[13 + JM_DOF[j]] = (T)c.pos[start_frame * 14 + JM_COL[j]];
-            st[30 + JM_DOF[j]] = (T)c.vel[vrow * 14 + JM_COL[j]];
+            st[13 + JM_DOF[j]] = (T)c.gpos()[start_frame * 14 + JM_COL[j]];
+            st[30 + JM_DOF[j]] = (T)c.gvel()[vrow * 14 + JM_COL[j]];
         }
     }
     for (int k = 0; k < 3; k++) { b.robot_pos[k] = 0; b.srp[k] = 0; }      // :277-281
@@ -402,8 +406,8 @@ __device__ __attribute__((always_inline)) void hier_reset_lane(const KArgs& a, i
         const int f0 = b.frame, f1 = b.frame + 1;
         const double qz = sin(th / 2), qw = cos(th / 2);
         const double r00 = -(qz * qz) + qw * qw, r01 = 2 * (0.0 - qz * qw), r10 = 2 * (0.0 + qz * qw), r11 = -(qz * qz) + qw * qw;
-        const double* e0 = c.ep + f0 * 27;
-        const double* e1 = c.ep + f1 * 27;
+        const HUM_GLOBAL double* e0 = c.gep() + f0 * 27;
+        const HUM_GLOBAL double* e1 = c.gep() + f1 * 27;
         const double l0x = r00 * e0[EP_RIGHT_LEG] + r01 * e0[EP_RIGHT_LEG + 1], l0y = r10 * e0[EP_RIGHT_LEG] + r11 * e0[EP_RIGHT_LEG + 1];
         const double l1x = r00 * e1[EP_RIGHT_LEG] + r01 * e1[EP_RIGHT_LEG + 1], l1y = r10 * e1[EP_RIGHT_LEG] + r11 * e1[EP_RIGHT_LEG + 1];
         if (init_vel) {
@@ -478,11 +482,11 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
         // updateReward (:494-522)
         double dJ = 0, dV = 0;
 #pragma unroll
-        for (int j = 0; j < NREF; j++) dJ = dJ + fabs(pp.q[JM_DOF[j]] - c.pos[b.frame * 14 + JM_COL[j]]) * JM_W[j];
+        for (int j = 0; j < NREF; j++) dJ = dJ + fabs(pp.q[JM_DOF[j]] - c.gpos()[b.frame * 14 + JM_COL[j]]) * JM_W[j];
         int vrow = b.frame;
         if (vrow >= c.n_vel) { vrow = c.n_vel - 1; ef |= HUM_EFLAG_VEL_ROW; }
 #pragma unroll
-        for (int j = 0; j < NREF; j++) dV = dV + fabs(pp.qd[JM_DOF[j]] - c.vel[vrow * 14 + JM_COL[j]]) * JM_WV[j];
+        for (int j = 0; j < NREF; j++) dV = dV + fabs(pp.qd[JM_DOF[j]] - c.gvel()[vrow * 14 + JM_COL[j]]) * JM_WV[j];
         const double jointScore = exp(4 * (-dJ / JOINT_WEIGHT_SUM));
         const double jointVelScore = exp((-dV / JOINT_VEL_WEIGHT_SUM) / 2);
         const double posture = exp(-((fabs(pp.yaw - b.hldt) + fabs(pp.roll)) + fabs(pp.pitch)));
@@ -796,7 +800,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
                     T q = T(0);
 #pragma unroll
                     for (int j = 0; j < NREF; j++)
-                        if (JM_DOF[j] == d) q = (T)c.pos[sf * 14 + JM_COL[j]];
+                        if (JM_DOF[j] == d) q = (T)c.gpos()[sf * 14 + JM_COL[j]];
                     T sn, cs;
                     hinge_sincos(q, &sn, &cs);
                     scs_r[2 * d] = sn;
@@ -926,7 +930,7 @@ __device__ inline void end_point_score(const KArgs& a, const T* st, const Book& 
     const double r11 = -(qz * qz) + qw * qw, r22 = qz * qz + qw * qw;
     constexpr int PART[4] = {10, 12, 17, 19}, EPC[4] = {6, 9, 0, 3};   // link0_11, right_foot, link0_18, left_foot
     constexpr double W[4] = {1, 3, 1, 3};
-    const double* e = c.ep + b.frame * 27;
+    const HUM_GLOBAL double* e = c.gep() + b.frame * 27;
     double d = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {

@@ -388,15 +388,19 @@ __device__ unsigned long long g_phase_cycles[32];
 #define PHASE_INIT unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
 #elif defined(HUM_WAVE_LOG)
 static __shared__ unsigned long long s_phase[24];
+static __shared__ unsigned long long s_tlast;   // shared: markers also sit inside the env-logic functions
 #define PHASE(k)                                                                 \
     do {                                                                         \
         if (threadIdx.x == 0) {                                                  \
             unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
-            s_phase[k] += t_ - t_last_;                                          \
-            t_last_ = t_;                                                        \
+            s_phase[k] += t_ - s_tlast;                                          \
+            s_tlast = t_;                                                        \
         }                                                                        \
     } while (0)
-#define PHASE_INIT unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
+#define PHASE_INIT                                                               \
+    do {                                                                         \
+        if (threadIdx.x == 0) s_tlast = __builtin_amdgcn_s_memtime();           \
+    } while (0)
 #elif defined(HUM_PHASE_MARK)   // static ISA attribution (tools/isa_phases.py): asm comments at phase ends
 #define PHASE(k) asm volatile("; @phase " #k ::: "memory")
 #define PHASE_INIT do { } while (0)

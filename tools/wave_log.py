@@ -79,7 +79,8 @@ for k in range(10):
     print("  %-12s %8.0f | %8.0f | %.2f" % (pn[k], ph[:, k].mean(), ph[top, k].mean(), np.corrcoef(ph[:, k], dur)[0, 1]))
 sub = X[:, 17:30]   # sub-phase markers 11-23 (HUM_SUBPHASE builds): time from the previous marker
 subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1: inertia+bias", 15: "pass3: base",
-        17: "post: book load", 18: "post: post_step"}
+        17: "post: book load", 19: "post: calc_state", 20: "post: reward", 21: "post: target",
+        22: "post: ref obs + done", 18: "post: outputs"}
 if sub.any():
     print("sub-phase cycles per block-step (each taken out of its phase above): mean | slowest 1%")
     for k, nm in subn.items():
