@@ -174,6 +174,12 @@ def _pools(a, dev, n, k, rank):
     return pool, hpool
 
 
+def launch_sizes(steps, k):
+    """Env steps per launch: whole launches of k, then one shorter launch for the remainder, so that exactly `steps`
+    env steps run (the driver's --steps need not be a multiple of k)."""
+    return [k] * (steps // k) + ([steps % k] if steps % k else [])
+
+
 def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     """Build the env, warm up, time `steps` env steps in launches of k.  Returns (env, wall_max_s, kernel_ms per
     env step, low_steps, gather_s, gathered)."""
@@ -182,10 +188,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     k = k or a.k
     if a.policy:
         k = 1   # closed loop: the policy acts on every step's observation
-    # launch sizes: whole launches of k env steps, then one shorter launch for the remainder, so exactly `steps`
-    # (and `warmup`) env steps run
-    sizes = [k] * (steps // k) + ([steps % k] if steps % k else [])
-    wsizes = [k] * (warmup // k) + ([warmup % k] if warmup % k else [])
+    sizes, wsizes = launch_sizes(steps, k), launch_sizes(warmup, k)
     launches, wlaunches = len(sizes), len(wsizes)
     pool, hpool = _pools(a, dev, n, k, rank)
     G = a.gather_every

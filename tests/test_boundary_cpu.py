@@ -73,3 +73,16 @@ def test_registration_seeds_are_distinct():
     assert {env_seed(_EnvContext({"seed": 5}, w, 0), 1024)[0] for w in range(7)} == {5}
     lanes = sorted(env_seed(_EnvContext({"seed": 5}, w, 0), 1024)[1] for w in range(7))
     assert all(b - a >= 1024 for a, b in zip(lanes, lanes[1:]))
+
+
+def test_bench_launch_sizes_cover_exactly_the_requested_steps():
+    """bench.py times exactly --steps env steps (the driver's contract) whatever --k is: whole launches of k, then
+    one shorter launch for the remainder."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for steps in (1, 7, 20, 31, 32, 33, 100, 1000):
+        for k in (1, 8, 32, 64):
+            sz = bench.launch_sizes(steps, k)
+            assert sum(sz) == steps and all(0 < x <= k for x in sz) and all(x == k for x in sz[:-1])
+    assert bench.launch_sizes(0, 32) == []
