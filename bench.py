@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--policy", action="store_true",
                     help="closed loop: actions from the on-GPU policy network (random-init weights, exploration "
                          "noise) inside the timed loop, SURVEY 8(f) rank 2")
+    ap.add_argument("--fused", action="store_true",
+                    help="with --policy: one hum_rollout_fused launch per --k steps (the policy inside the env kernel) "
+                         "instead of a policy launch + an env launch per step")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / parity side measurements")
     return ap.parse_args()
 
@@ -186,8 +189,6 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     import torch
     import torch.distributed as dist
     k = k or a.k
-    if a.policy:
-        k = 1   # closed loop: the policy acts on every step's observation
     sizes, wsizes = launch_sizes(steps, k), launch_sizes(warmup, k)
     launches, wlaunches = len(sizes), len(wsizes)
     pool, hpool = _pools(a, dev, n, k, rank)
@@ -225,6 +226,9 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             def step(s, kk=1):
                 pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s, out=actbuf)
                 return env.step(actbuf, autoreset=True)
+            if k > 1:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
+                def step(s, kk=k):
+                    return pol.rollout(env, kk, explore=True, step0=s * k, trajectories=True, fused=True)
     env.reset()
     env.done.zero_()
     for w in range(wlaunches):
@@ -330,8 +334,8 @@ def main():
     if a.hier:
         from ilrl_amd.hier_env import HIER_CLIP
         a.clip = HIER_CLIP
-    if a.policy:
-        a.k = 1
+    if a.policy and not a.fused:
+        a.k = 1   # closed loop: the policy acts on every step's observation, one launch each
     if a.k < 1:
         raise SystemExit("--k must be >= 1")
     env, wall_max, kern_ms, low_steps, gather_s, gathered = run(a, world, rank, dev, n, a.precision, a.steps, a.warmup,

@@ -811,6 +811,63 @@ int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
 
 }  // extern "C"
 __attribute__((visibility("hidden"))) int hum_internal_device(const hum_env* e) { return e ? e->cfg.device : -1; }
+// hum_rollout_fused (policy.hip): k sampler steps in one launch of the fused-policy cooperative kernel.  pw: the
+// hum_policy weight block.  Missing rew / done traces go to temporary buffers (the call then synchronises).
+__attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
+    hum_env* e, const float* pw, uint64_t seed, int32_t k, int32_t explore, uint64_t step0, float* obs, float* obs_reset,
+    uint8_t* done, float* reward, float* act_last, float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj,
+    void* stream) {
+    if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != 4 || e->terrain != HUM_TERRAIN_PLANE ||
+        e->cfg.hier)
+        return fail(HUM_ERR_STATE, "hum_rollout_fused: needs the cooperative fp32 kernel, 4 envs per block, plane ground "
+                                   "and the low-level env (use hum_rollout)");
+    if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_rollout_fused: no clip uploaded (hum_set_clip)");
+    HIPCHK(hipSetDevice(e->cfg.device));
+    const hipStream_t s = stream_of(e, stream);
+    const size_t kn = (size_t)k * e->n;
+    float* rt = rew_traj;
+    uint8_t* dt = done_traj;
+    bool tmp = false;
+    if (!rt || !dt) {
+        tmp = true;
+        if (!rt) HIPCHK(hipMalloc((void**)&rt, kn * sizeof(float)));
+        if (!dt) HIPCHK(hipMalloc((void**)&dt, kn));
+    }
+    KArgs a = make_args(e);
+    a.flags = HUM_STEP_AUTORESET;
+    a.ksteps = k;
+    a.obs = obs;
+    a.obs_reset = obs_reset;
+    a.done_in = done;
+    a.rew = rt;
+    a.done = dt;
+    a.frame_out = nullptr;
+    a.act = nullptr;
+    a.pw = pw;
+    a.pseed = seed;
+    a.pstep0 = step0;
+    a.pexplore = explore;
+    a.obs_traj = obs_traj;
+    a.act_traj = act_traj;
+    a.act_last = act_last;
+    const int nb = (e->n + 3) / 4;
+#ifndef HUM_DIAG_F32_ONLY
+    hipError_t st = launch_group_f32_4_policy(a, nb, s);
+#else   // diagnostic builds link the benchmarked kernel's phase-timed copy only
+    (void)nb;
+    hipError_t st = hipErrorInvalidDeviceFunction;
+#endif
+    if (st == hipSuccess) st = hipMemcpyAsync(reward, rt + (k - 1) * (size_t)e->n, (size_t)e->n * sizeof(float),
+                                              hipMemcpyDeviceToDevice, s);
+    if (st == hipSuccess) st = hipMemcpyAsync(done, dt + (k - 1) * (size_t)e->n, (size_t)e->n, hipMemcpyDeviceToDevice, s);
+    if (tmp) {
+        if (st == hipSuccess) st = hipStreamSynchronize(s);
+        if (rt != rew_traj) (void)hipFree(rt);
+        if (dt != done_traj) (void)hipFree(dt);
+    }
+    if (st != hipSuccess) return fail(HUM_ERR_HIP, std::string("hum_rollout_fused: ") + hipGetErrorString(st));
+    return HUM_OK;
+}
 extern "C" {
 
 

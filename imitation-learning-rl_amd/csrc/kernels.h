@@ -68,6 +68,16 @@ struct KArgs {
     // multi-step launch (hum_step_k / hum_hier_step_k): env steps per launch; the per-step inputs and outputs
     // above are then [ksteps, n, ...] arrays, step-major: lane i's row of step t is io = t * n + i
     int ksteps;
+    // fused rollout (hum_rollout_fused, POLICY kernels): the policy network acts inside the step loop.  pw = the
+    // hum_policy weight block (w1 [72][256] with rows 70, 71 zero, b1 [256], w2 [256][256], b2 [256], w3 [256][17],
+    // b3 [17], log_std [17]); done_in = the previous step's done flags (step 0 input); per-step traces [k, n, ...]
+    const float* pw;
+    const unsigned char* done_in;
+    float* obs_traj;
+    float* act_traj;
+    float* act_last;                // [n,17] the last step's clipped actions (hum_rollout's act_buf)
+    unsigned long long pseed, pstep0;
+    int pexplore;
 };
 
 // CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
@@ -651,13 +661,131 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
     if (ef) atomicOr(a.eflags, ef);
 }
 
+// ----------------------------------------------------------------------------------- fused policy
+// The policy network of policy.hip (RLlib FCNet 70-256-256-17 tanh + DiagGaussian sample + clip_actions) for the
+// EPB_ envs of a wave, evaluated by all 64 lanes before the step's physics: lane l owns hidden units l + 64 m
+// (m < 4) of every env, each a k-ordered fmaf chain from 0 (the order policy.hip's v_mfma_f32_16x16x4_f32 tiles
+// accumulate in), then tanhf(acc + bias); the output layer's 17 x EPB_ dot products go to lanes (env, column).
+// Scratch (float units past the env's ABA transients, dead before the physics): input row, h1, h2, actions.
+constexpr int PX_OFF = 0, PH1_OFF = 72, PH2_OFF = 328, PACT_OFF = 584, PSCR = 608;
+template <typename T>
+__device__ __attribute__((always_inline)) inline float* policy_scratch(GroupLDS<T>& S) {
+    static_assert(sizeof(S.x) >= sizeof(S.x.aba) + PSCR * sizeof(float), "policy scratch");
+    return reinterpret_cast<float*>(reinterpret_cast<char*>(&S.x) + sizeof(S.x.aba));
+}
+__device__ inline unsigned long long pmix64(unsigned long long z) {   // policy.hip's mix64
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+template <typename T, int EPB_>
+__device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, GroupLDS<T>* sh, int blk, int t) {
+    const int lane = threadIdx.x & 63;
+    const HUM_GLOBAL float* W1 = (const HUM_GLOBAL float*)a.pw;
+    const HUM_GLOBAL float* B1 = W1 + 72 * 256;
+    const HUM_GLOBAL float* W2 = B1 + 256;
+    const HUM_GLOBAL float* B2 = W2 + 256 * 256;
+    const HUM_GLOBAL float* W3 = B2 + 256;
+    const HUM_GLOBAL float* B3 = W3 + 256 * HUM_NACT;
+    const HUM_GLOBAL float* LSTD = B3 + HUM_NACT;
+    float* F[EPB_];
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) F[e] = policy_scratch(sh[e]);
+    {   // hidden layer 1 (K = 70: policy.hip's zero rows 70, 71 add exact zeros)
+        float acc[EPB_][4];
+#pragma unroll
+        for (int e = 0; e < EPB_; e++)
+#pragma unroll
+            for (int m = 0; m < 4; m++) acc[e][m] = 0.f;
+#pragma unroll 2
+        for (int k = 0; k < HUM_NOBS; k++) {
+            float w[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) w[m] = W1[k * 256 + lane + 64 * m];
+#pragma unroll
+            for (int e = 0; e < EPB_; e++) {
+                const float x = F[e][PX_OFF + k];
+#pragma unroll
+                for (int m = 0; m < 4; m++) acc[e][m] = fmaf(x, w[m], acc[e][m]);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const float bias = B1[lane + 64 * m];
+#pragma unroll
+            for (int e = 0; e < EPB_; e++) F[e][PH1_OFF + lane + 64 * m] = tanhf(acc[e][m] + bias);
+        }
+    }
+    wave_sync();
+    {   // hidden layer 2
+        float acc[EPB_][4];
+#pragma unroll
+        for (int e = 0; e < EPB_; e++)
+#pragma unroll
+            for (int m = 0; m < 4; m++) acc[e][m] = 0.f;
+#pragma unroll 2
+        for (int k = 0; k < 256; k++) {
+            float w[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) w[m] = W2[k * 256 + lane + 64 * m];
+#pragma unroll
+            for (int e = 0; e < EPB_; e++) {
+                const float x = F[e][PH1_OFF + k];
+#pragma unroll
+                for (int m = 0; m < 4; m++) acc[e][m] = fmaf(x, w[m], acc[e][m]);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const float bias = B2[lane + 64 * m];
+#pragma unroll
+            for (int e = 0; e < EPB_; e++) F[e][PH2_OFF + lane + 64 * m] = tanhf(acc[e][m] + bias);
+        }
+    }
+    wave_sync();
+    // output layer + DiagGaussian sample + clip_actions: (env, column) pairs, 16 columns per pass over the lanes
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+        const int e = pass == 0 ? lane >> 4 : lane, c = pass == 0 ? (lane & 15) : 16;
+        if (e < EPB_ && (pass == 0 || lane < EPB_)) {
+            float acc = 0.f;
+            const float* h2 = F[0] + PH2_OFF;
+#pragma unroll
+            for (int q = 1; q < EPB_; q++) h2 = e == q ? F[q] + PH2_OFF : h2;
+#pragma unroll 4
+            for (int k = 0; k < 256; k++) acc = fmaf(h2[k], W3[k * HUM_NACT + c], acc);
+            const float mean = acc + B3[c];
+            float v = mean;
+            const int i = blk * EPB_ + e;
+            if (a.pexplore) {   // policy.hip: (seed, lane, step, column) through separate mixing rounds, Box-Muller
+                const unsigned long long x = pmix64(pmix64(pmix64(a.pseed ^ (unsigned long long)i) ^ (a.pstep0 + t)) ^
+                                                    (unsigned long long)c);
+                const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;
+                const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
+                v = mean + expf(LSTD[c]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+            }
+            float* pa = F[0] + PACT_OFF;
+#pragma unroll
+            for (int q = 1; q < EPB_; q++) pa = e == q ? F[q] + PACT_OFF : pa;
+            pa[c] = fminf(fmaxf(v, -1.f), 1.f);
+            if (i < a.n) {
+                const long io = (long)t * a.n + i;
+                if (a.act_traj) a.act_traj[io * HUM_NACT + c] = v;   // the sample before clip_actions (SampleBatch)
+                if (a.act_last && t == a.ksteps - 1) a.act_last[(long)i * HUM_NACT + c] = pa[c];
+            }
+        }
+    }
+    wave_sync();
+}
+
 // Cooperative step: 16 lanes per env, EPB_ envs per block of EPB_*16 threads (one wavefront), env working
 // set in LDS.  EPB_ = 4 fills the wave; EPB_ = 2 leaves half of it idle but lets a SIMD hold two waves
 // (19.3 KB LDS per block), so one wave's LDS/memory waits overlap the other's VALU issue.
 #ifndef HUM_GROUP_MIN_WAVES
 #define HUM_GROUP_MIN_WAVES 1
 #endif
-template <typename T, int EPB_, bool TERRAIN = false>
+template <typename T, int EPB_, bool TERRAIN = false, bool POLICY = false>
 __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a0) {
     __shared__ GroupLDS<T> sh[EPB_];
     const int ksteps = a0.ksteps;
@@ -691,6 +819,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     }
     __syncthreads();
     unsigned ef = 0;
+    bool prev_reset = false;   // POLICY: the env auto-reset at the previous step (its next input is the reset obs)
 #pragma unroll 1
     for (int t = 0; t < ksteps; t++) {
     // Everything the step body derives from the launch arguments or the lane index is recomputed in every step:
@@ -710,9 +839,44 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     int* carry = reinterpret_cast<int*>(&S.tau[NDOF]);
     const int gbit = (tid & 63) & ~(GL - 1);
     const long io = (long)t * a.n + i;   // this step's input / output row of the env
+    if constexpr (POLICY) {
+        // the sampler's input: step 0 the handle's current observation (a lane done at the previous step: its reset
+        // observation), later steps the row the previous step staged (its reset row if it reset)
+        float* X = policy_scratch(S) + PX_OFF;
+        const float* src = nullptr;
+        if (t == 0) {
+            if (valid) src = ((a.done_in && a.done_in[i]) ? a.obs_reset : a.obs) + (long)i * HUM_NOBS;
+        } else {
+            src = reinterpret_cast<const float*>(&S.x.aba.IA[0][0] + (prev_reset ? 144 : 72));
+        }
+        float xv[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const int k = l + GL * j;
+            xv[j] = (valid && k < HUM_NOBS) ? src[k] : 0.f;
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const int k = l + GL * j;
+            if (k < HUM_NOBS) {
+                X[k] = xv[j];
+                if (valid && a.obs_traj) a.obs_traj[io * HUM_NOBS + k] = xv[j];
+            }
+        }
+        wave_sync();
+        policy_wave<T, EPB_>(a, sh, blk, t);
+    }
+    // POLICY: the env's clipped actions held in registers across the physics (which reuses the scratch), one per lane
+    // (lane 0 also the 17th); post_step reads them back from LDS for the electricity cost
+    float pact0 = 0.f, pact1 = 0.f;
+    if constexpr (POLICY) {
+        pact0 = policy_scratch(S)[PACT_OFF + l];
+        pact1 = policy_scratch(S)[PACT_OFF + GL];
+    }
     bool fin = true;
     for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60)
-        const float av = valid ? a.act[io * HUM_NACT + k] : 0.f;
+        const float av = !valid ? 0.f : (POLICY ? policy_scratch(S)[PACT_OFF + k] : a.act[io * HUM_NACT + k]);
         fin = fin && isfinite(av);
         S.tau[M.act_dof[k]] = (T)motor_torque(a.np1, M.act_gain[k], M.act_gain_d[k], isfinite(av) ? av : 0.f);
     }
@@ -749,6 +913,10 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     float* rstage = reinterpret_cast<float*>(scs + 144);   // the auto-reset observation
     static_assert(sizeof(sh[0].x.aba.IA) >= (144 + HUM_NOBS) * sizeof(T) && 2 * NDOF + 2 + 2 * NDOF <= 72,
                   "output row staging");
+    if constexpr (POLICY) {   // the step's actions for post_step, in the reset-obs staging row (written after it)
+        rstage[l] = pact0;
+        if (l == 0) rstage[GL] = pact1;
+    }
     wave_sync();
     PHASE_INIT;
     Book b;
@@ -774,7 +942,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             } else {
                 float act[HUM_NACT];
 #pragma unroll
-                for (int k = 0; k < HUM_NACT; k++) act[k] = a.act[io * HUM_NACT + k];
+                for (int k = 0; k < HUM_NACT; k++) act[k] = POLICY ? rstage[k] : a.act[io * HUM_NACT + k];
                 post_step(a, i, io, st, b, act, ef, scs, &rst, ostage);
             }
         }
@@ -821,14 +989,18 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             store_book(a, i, b);
         }
         wave_sync();
-        if (valid) {   // the output rows, coalesced
-            float* orow = a.obs + io * HUM_NOBS;
+        // the output rows, coalesced (POLICY: the next step's input stays in LDS; only the last step's rows go to
+        // the handle's [n, 70] obs / obs_reset buffers)
+        const long orow_i = POLICY ? (long)i : io;
+        if (valid && (!POLICY || t == ksteps - 1)) {
+            float* orow = a.obs + orow_i * HUM_NOBS;
             for (int k = l; k < HUM_NOBS; k += GL) orow[k] = ostage[k];
             if (sf >= 0 && a.obs_reset) {
-                float* rrow = a.obs_reset + io * HUM_NOBS;
+                float* rrow = a.obs_reset + orow_i * HUM_NOBS;
                 for (int k = l; k < HUM_NOBS; k += GL) rrow[k] = rstage[k];
             }
         }
+        prev_reset = sf >= 0;
     }
     PHASE(10);
     if (valid && l == 0 && booked) {   // the per-env integers the next step's lanes read
@@ -993,5 +1165,6 @@ __global__ void parts_kernel(KArgs a, double* out) {
 
 // the benchmarked cooperative kernel lives in its own translation unit (group_f32.hip)
 hipError_t launch_group_f32_4(const KArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_group_f32_4_policy(const KArgs& a, int nblocks, hipStream_t s);
 
 }  // namespace hkk

@@ -23,6 +23,9 @@
 
 void hum_internal_set_error(const char* msg);
 int hum_internal_device(const hum_env* env);   // humanoid_env.hip
+int hum_internal_rollout_fused(hum_env* e, const float* pw, uint64_t seed, int32_t k, int32_t explore, uint64_t step0,
+                               float* obs, float* obs_reset, uint8_t* done, float* reward, float* act_last,
+                               float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj, void* stream);
 
 namespace {
 
@@ -268,6 +271,17 @@ int hum_rollout(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_
             return perr(HUM_ERR_HIP, "hum_rollout: done copy");
     }
     return HUM_OK;
+}
+
+int hum_rollout_fused(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_t step0, float* obs,
+                      float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
+                      float* rew_traj, uint8_t* done_traj, void* stream) {
+    if (!env || !p || k <= 0 || !obs || !obs_reset || !done || !reward || !act_buf)
+        return perr(HUM_ERR_ARG, "hum_rollout_fused: bad argument");
+    if (hum_internal_device(env) != p->device)
+        return perr(HUM_ERR_ARG, "hum_rollout_fused: the env handle and the policy are on different devices");
+    return hum_internal_rollout_fused(env, p->w, p->seed, k, explore, step0, obs, obs_reset, done, reward, act_buf,
+                                      obs_traj, act_traj, rew_traj, done_traj, stream);
 }
 
 }  // extern "C"

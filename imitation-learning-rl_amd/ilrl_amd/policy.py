@@ -99,11 +99,12 @@ class DevicePolicy:
                 "hum_policy_act")
         return act
 
-    def rollout(self, venv, k, explore=True, step0=0, trajectories=True):
+    def rollout(self, venv, k, explore=True, step0=0, trajectories=True, fused=False):
         """k sampler steps (policy -> env step with auto-reset) on venv's lanes, all on the device with no host
         round trip.  venv.obs must hold the current observation (after venv.reset()).  Returns the trajectory
         tensors {obs [k,n,70] (policy inputs), actions [k,n,17] (the samples before clip_actions, as RLlib records
-        them), rewards [k,n], dones [k,n]} (or {})."""
+        them), rewards [k,n], dones [k,n]} (or {}).  fused: one launch with the policy inside the step kernel
+        (hum_rollout_fused; cooperative fp32 handles with 4 envs per block on the plane)."""
         t = self.torch
         n = venv.n
         if not hasattr(venv, "_act_buf"):
@@ -115,10 +116,11 @@ class DevicePolicy:
                   "rewards": t.empty(k, n, dtype=t.float32, device=venv.device),
                   "dones": t.empty(k, n, dtype=t.uint8, device=venv.device)}
         p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
-        N.check(N.lib().hum_rollout(venv.h, self.h, k, int(bool(explore)), ctypes.c_uint64(step0), p(venv.obs),
-                                    p(venv.obs_reset), p(venv.done), p(venv.reward), p(venv._act_buf),
-                                    p(tr.get("obs")), p(tr.get("actions")), p(tr.get("rewards")), p(tr.get("dones")),
-                                    venv._stream()), "hum_rollout")
+        fn = N.lib().hum_rollout_fused if fused else N.lib().hum_rollout
+        N.check(fn(venv.h, self.h, k, int(bool(explore)), ctypes.c_uint64(step0), p(venv.obs),
+                   p(venv.obs_reset), p(venv.done), p(venv.reward), p(venv._act_buf),
+                   p(tr.get("obs")), p(tr.get("actions")), p(tr.get("rewards")), p(tr.get("dones")),
+                   venv._stream()), "hum_rollout_fused" if fused else "hum_rollout")
         return tr
 
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 8
+#define HUM_ABI_VERSION 9
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -321,6 +321,16 @@ int hum_policy_act_ex(hum_policy* policy, const float* obs, const float* obs_res
 int hum_rollout(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
                 float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
                 float* rew_traj, uint8_t* done_traj, void* stream);
+/* hum_rollout in ONE launch: the policy network is evaluated inside the multi-step env kernel (per wave, before
+ * each step's physics), so the k steps keep their state in LDS and the launch's slowest-wave tail is paid once per k
+ * steps instead of once per step.  Same arguments and outputs as hum_rollout (act_buf receives the last step's
+ * clipped actions; obs / obs_reset / done / reward end as the last step left them).  The policy arithmetic is the
+ * same k-ordered fp32 fma chains; the physics is the benchmarked kernel's.  Needs a handle with the cooperative fp32
+ * kernel, 4 envs per block, plane ground and the low-level env (HUM_ERR_STATE otherwise: use hum_rollout).
+ * Replaces: the RLlib sampler's compute_actions -> env.step loop (train_config.py:107-111, low_level_env.py:475). */
+int hum_rollout_fused(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
+                      float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
+                      float* rew_traj, uint8_t* done_traj, void* stream);
 
 /* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
 int hum_get_aux(hum_env* env, float* aux_out, void* stream);

@@ -88,6 +88,57 @@ def test_rollout_equals_python_loop():
     pol.close()
 
 
+@pytest.mark.parametrize("k", [1, 16])
+def test_fused_rollout_equals_policy_kernel_and_step_k(k):
+    """hum_rollout_fused (the policy inside the multi-step env kernel) vs its two halves run separately: every
+    recorded sample equals the standalone policy kernel's on the recorded input (the same k-ordered fp32 fma
+    chains), and replaying the clipped samples through hum_step_k from the same start state reproduces the recorded
+    rewards, dones, next inputs and final state bitwise."""
+    n = 512
+    pol = DevicePolicy.random_init(seed=9)
+    envs = [HumanoidVecEnv(n, clips=("motion02_04",), seed=2) for _ in range(2)]
+    for e in envs:
+        e.done.fill_(1)
+        e.reset()
+    tr = pol.rollout(envs[0], k, explore=True, step0=100, fused=True)
+    act = torch.empty(n, 17, device="cuda")
+    raw = torch.empty(n, 17, device="cuda")
+    worst = 0.0
+    for t in range(k):
+        pol.act(tr["obs"][t], explore=True, step=100 + t, out=act, raw_out=raw)
+        worst = max(worst, (tr["actions"][t] - raw).abs().max().item())
+    print("fused policy vs policy kernel: max |sample diff| %.3g" % worst)
+    assert worst == 0.0
+    torch.testing.assert_close(envs[0]._act_buf, tr["actions"][k - 1].clamp(-1, 1), atol=0, rtol=0)
+    e = envs[1]
+    obs_k, rew_k, done_k, _, rst_k = e.step_k(tr["actions"].clamp(-1, 1).contiguous(), autoreset=True)
+    torch.testing.assert_close(tr["rewards"], rew_k, atol=0, rtol=0)
+    assert torch.equal(tr["dones"], done_k)
+    for t in range(k - 1):
+        want = torch.where(done_k[t].bool()[:, None], rst_k[t], obs_k[t])
+        torch.testing.assert_close(tr["obs"][t + 1], want, atol=0, rtol=0)
+    torch.testing.assert_close(envs[0].obs, obs_k[k - 1], atol=0, rtol=0)
+    torch.testing.assert_close(envs[0].reward, rew_k[k - 1], atol=0, rtol=0)
+    assert torch.equal(envs[0].done, done_k[k - 1])
+    p0, b0 = envs[0].get_state()
+    p1, b1 = e.get_state()
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(b0, b1)
+    for x in envs:
+        x.close()
+    pol.close()
+
+
+def test_fused_rollout_rejects_other_kernels():
+    pol = DevicePolicy.random_init(seed=1)
+    env = HumanoidVecEnv(64, clips=("motion02_04",), seed=2, precision="fp64")
+    env.reset()
+    with pytest.raises(N.NativeError, match="hum_rollout_fused"):
+        pol.rollout(env, 4, fused=True)
+    env.close()
+    pol.close()
+
+
 def test_rllib_weight_names():
     """from_rllib_weights picks the policy branch of an RLlib 1.2 TF FullyConnectedNetwork weight dict."""
     rng = np.random.default_rng(0)
