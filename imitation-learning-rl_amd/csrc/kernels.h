@@ -663,10 +663,12 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
 
 // ----------------------------------------------------------------------------------- fused policy
 // The policy network of policy.hip (RLlib FCNet 70-256-256-17 tanh + DiagGaussian sample + clip_actions) for the
-// EPB_ envs of a wave, evaluated by all 64 lanes before the step's physics: lane l owns hidden units l + 64 m
-// (m < 4) of every env, each a k-ordered fmaf chain from 0 (the order policy.hip's v_mfma_f32_16x16x4_f32 tiles
-// accumulate in), then tanhf(acc + bias); the output layer's 17 x EPB_ dot products go to lanes (env, column).
-// Scratch (float units past the env's ABA transients, dead before the physics): input row, h1, h2, actions.
+// EPB_ envs of a wave, evaluated by all 64 lanes before the step's physics: lane l owns hidden units 4 l + m
+// (m < 4) of every env (one 16-byte weight load per k, two v_pk_fma_f32 per env), each a k-ordered fma chain
+// from 0 (the order policy.hip's v_mfma_f32_16x16x4_f32 tiles accumulate in), then tanhf(acc + bias); the output layer's 16 x EPB_ (env, column)
+// chains go one to a lane, the 17th column's EPB_ chains ride along in lanes < EPB_ (one pass).  One wave per SIMD
+// cannot hide the L2 latency of the weight loads, so the k loops are unrolled deep enough to keep 10-16 loads in
+// flight.  Scratch (float units past the env's ABA transients, dead before the physics): input row, h1, h2, actions.
 constexpr int PX_OFF = 0, PH1_OFF = 72, PH2_OFF = 328, PACT_OFF = 584, PSCR = 608;
 template <typename T>
 __device__ __attribute__((always_inline)) inline float* policy_scratch(GroupLDS<T>& S) {
@@ -679,8 +681,50 @@ __device__ inline unsigned long long pmix64(unsigned long long z) {   // policy.
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+typedef float pf4 __attribute__((ext_vector_type(4)));
+// one hidden layer: F[e][dst + 4 lane + m] = tanh(sum_k F[e][src + k] W[k][4 lane + m] + B[4 lane + m])
+template <int EPB_, int K, int UNROLL>
+__device__ __attribute__((always_inline)) inline void policy_hidden(float* const (&F)[EPB_], const HUM_GLOBAL float* W,
+                                                                    const HUM_GLOBAL float* B, int src, int dst,
+                                                                    int lane) {
+    float acc[EPB_][4];
+#pragma unroll
+    for (int e = 0; e < EPB_; e++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[e][m] = 0.f;
+    // packed: v_pk_fma_f32 does units (4 lane, 4 lane + 1) and (4 lane + 2, 4 lane + 3) of an env in one op each
+    typedef float pf2 __attribute__((ext_vector_type(2)));
+    pf2 pacc[EPB_][2];
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) pacc[e][0] = pacc[e][1] = pf2{0.f, 0.f};
+#pragma unroll UNROLL
+    for (int k = 0; k < K; k++) {
+        const pf4 w = *reinterpret_cast<const HUM_GLOBAL pf4*>(W + k * 256 + 4 * lane);
+        const pf2 w01 = {w[0], w[1]}, w23 = {w[2], w[3]};
+#pragma unroll
+        for (int e = 0; e < EPB_; e++) {
+            const float x = F[e][src + k];
+            const pf2 xx = {x, x};
+            pacc[e][0] = __builtin_elementwise_fma(xx, w01, pacc[e][0]);
+            pacc[e][1] = __builtin_elementwise_fma(xx, w23, pacc[e][1]);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) {
+        acc[e][0] = pacc[e][0][0];
+        acc[e][1] = pacc[e][0][1];
+        acc[e][2] = pacc[e][1][0];
+        acc[e][3] = pacc[e][1][1];
+    }
+    const pf4 bias = *reinterpret_cast<const HUM_GLOBAL pf4*>(B + 4 * lane);
+#pragma unroll
+    for (int e = 0; e < EPB_; e++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) F[e][dst + 4 * lane + m] = tanhf(acc[e][m] + bias[m]);
+}
 template <typename T, int EPB_>
 __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, GroupLDS<T>* sh, int blk, int t) {
+    static_assert(EPB_ * 16 == 64, "policy_wave: one (env, column) chain per lane");
     const int lane = threadIdx.x & 63;
     const HUM_GLOBAL float* W1 = (const HUM_GLOBAL float*)a.pw;
     const HUM_GLOBAL float* B1 = W1 + 72 * 256;
@@ -692,90 +736,51 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
     float* F[EPB_];
 #pragma unroll
     for (int e = 0; e < EPB_; e++) F[e] = policy_scratch(sh[e]);
-    {   // hidden layer 1 (K = 70: policy.hip's zero rows 70, 71 add exact zeros)
-        float acc[EPB_][4];
-#pragma unroll
-        for (int e = 0; e < EPB_; e++)
-#pragma unroll
-            for (int m = 0; m < 4; m++) acc[e][m] = 0.f;
-#pragma unroll 2
-        for (int k = 0; k < HUM_NOBS; k++) {
-            float w[4];
-#pragma unroll
-            for (int m = 0; m < 4; m++) w[m] = W1[k * 256 + lane + 64 * m];
-#pragma unroll
-            for (int e = 0; e < EPB_; e++) {
-                const float x = F[e][PX_OFF + k];
-#pragma unroll
-                for (int m = 0; m < 4; m++) acc[e][m] = fmaf(x, w[m], acc[e][m]);
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            const float bias = B1[lane + 64 * m];
-#pragma unroll
-            for (int e = 0; e < EPB_; e++) F[e][PH1_OFF + lane + 64 * m] = tanhf(acc[e][m] + bias);
-        }
-    }
+    // hidden layer 1 (K = 70: policy.hip's zero rows 70, 71 add exact zeros), hidden layer 2
+    policy_hidden<EPB_, HUM_NOBS, 10>(F, W1, B1, PX_OFF, PH1_OFF, lane);
     wave_sync();
-    {   // hidden layer 2
-        float acc[EPB_][4];
-#pragma unroll
-        for (int e = 0; e < EPB_; e++)
-#pragma unroll
-            for (int m = 0; m < 4; m++) acc[e][m] = 0.f;
-#pragma unroll 2
-        for (int k = 0; k < 256; k++) {
-            float w[4];
-#pragma unroll
-            for (int m = 0; m < 4; m++) w[m] = W2[k * 256 + lane + 64 * m];
-#pragma unroll
-            for (int e = 0; e < EPB_; e++) {
-                const float x = F[e][PH1_OFF + k];
-#pragma unroll
-                for (int m = 0; m < 4; m++) acc[e][m] = fmaf(x, w[m], acc[e][m]);
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            const float bias = B2[lane + 64 * m];
-#pragma unroll
-            for (int e = 0; e < EPB_; e++) F[e][PH2_OFF + lane + 64 * m] = tanhf(acc[e][m] + bias);
-        }
-    }
+    policy_hidden<EPB_, 256, 16>(F, W2, B2, PH1_OFF, PH2_OFF, lane);
     wave_sync();
-    // output layer + DiagGaussian sample + clip_actions: (env, column) pairs, 16 columns per pass over the lanes
+    // output layer: chain A = (env lane / 16, column lane % 16), chain B = (env lane, column 16) in lanes < EPB_
+    const int eA = lane >> 4, cA = lane & 15, eB = lane < EPB_ ? lane : 0;
+    const float* hA = F[0] + PH2_OFF;
+    const float* hB = F[0] + PH2_OFF;
 #pragma unroll
-    for (int pass = 0; pass < 2; pass++) {
-        const int e = pass == 0 ? lane >> 4 : lane, c = pass == 0 ? (lane & 15) : 16;
-        if (e < EPB_ && (pass == 0 || lane < EPB_)) {
-            float acc = 0.f;
-            const float* h2 = F[0] + PH2_OFF;
-#pragma unroll
-            for (int q = 1; q < EPB_; q++) h2 = e == q ? F[q] + PH2_OFF : h2;
-#pragma unroll 4
-            for (int k = 0; k < 256; k++) acc = fmaf(h2[k], W3[k * HUM_NACT + c], acc);
-            const float mean = acc + B3[c];
-            float v = mean;
-            const int i = blk * EPB_ + e;
-            if (a.pexplore) {   // policy.hip: (seed, lane, step, column) through separate mixing rounds, Box-Muller
-                const unsigned long long x = pmix64(pmix64(pmix64(a.pseed ^ (unsigned long long)i) ^ (a.pstep0 + t)) ^
-                                                    (unsigned long long)c);
-                const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;
-                const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
-                v = mean + expf(LSTD[c]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
-            }
-            float* pa = F[0] + PACT_OFF;
-#pragma unroll
-            for (int q = 1; q < EPB_; q++) pa = e == q ? F[q] + PACT_OFF : pa;
-            pa[c] = fminf(fmaxf(v, -1.f), 1.f);
-            if (i < a.n) {
-                const long io = (long)t * a.n + i;
-                if (a.act_traj) a.act_traj[io * HUM_NACT + c] = v;   // the sample before clip_actions (SampleBatch)
-                if (a.act_last && t == a.ksteps - 1) a.act_last[(long)i * HUM_NACT + c] = pa[c];
-            }
-        }
+    for (int q = 1; q < EPB_; q++) {
+        hA = eA == q ? F[q] + PH2_OFF : hA;
+        hB = eB == q ? F[q] + PH2_OFF : hB;
     }
+    float accA = 0.f, accB = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < 256; k++) {
+        const HUM_GLOBAL float* wr = W3 + k * HUM_NACT;
+        accA = fmaf(hA[k], wr[cA], accA);
+        accB = fmaf(hB[k], wr[16], accB);
+    }
+    // + DiagGaussian sample + clip_actions
+    auto finish = [&](int e, int c, float acc) {
+        const float mean = acc + B3[c];
+        float v = mean;
+        const int i = blk * EPB_ + e;
+        if (a.pexplore) {   // policy.hip: (seed, lane, step, column) through separate mixing rounds, Box-Muller
+            const unsigned long long x = pmix64(pmix64(pmix64(a.pseed ^ (unsigned long long)i) ^ (a.pstep0 + t)) ^
+                                                (unsigned long long)c);
+            const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;
+            const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
+            v = mean + expf(LSTD[c]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+        }
+        float* pa = F[0] + PACT_OFF;
+#pragma unroll
+        for (int q = 1; q < EPB_; q++) pa = e == q ? F[q] + PACT_OFF : pa;
+        pa[c] = fminf(fmaxf(v, -1.f), 1.f);
+        if (i < a.n) {
+            const long io = (long)t * a.n + i;
+            if (a.act_traj) a.act_traj[io * HUM_NACT + c] = v;   // the sample before clip_actions (SampleBatch)
+            if (a.act_last && t == a.ksteps - 1) a.act_last[(long)i * HUM_NACT + c] = pa[c];
+        }
+    };
+    finish(eA, cA, accA);
+    if (lane < EPB_) finish(eB, 16, accB);
     wave_sync();
 }
 
