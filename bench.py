@@ -56,6 +56,8 @@ def parse():
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: host-staged, tests)")
     ap.add_argument("--dump-gather", default=None,
                     help="rank 0: save every gathered trajectory fragment to this .npz (tests)")
+    ap.add_argument("--dump-lane-stride", type=int, default=1,
+                    help="with --dump-gather: keep every S-th global lane only (bounds host memory at 32768 lanes)")
     ap.add_argument("--policy", action="store_true",
                     help="closed loop: actions from the on-GPU policy network (random-init weights, exploration "
                          "noise) inside the timed loop, SURVEY 8(f) rank 2")
@@ -160,6 +162,15 @@ def parity_sample(env, clips, per_clip=64, seed=5, sens_bound=1e-5):
                             "state_max_abs_err": float(max(s64)), "done_mismatches": dm64}}
 
 
+def _actions_desc(a):
+    if a.hier and a.policy:
+        return ("on-GPU policies of both levels in the loop (random-init 44-256-256-2 high-level and 70-256-256-17 "
+                "low-level tanh MLPs + Gaussian exploration, hum_hier_rollout)")
+    if a.policy:
+        return "on-GPU policy actions (random-init 70-256-256-17 tanh MLP + Gaussian exploration) in the loop"
+    return "uniform random actions (a fresh row per env step)"
+
+
 def _load_json(path):
     try:
         return json.load(open(os.path.join(REPO, path)))
@@ -185,7 +196,7 @@ def launch_sizes(steps, k):
 
 def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     """Build the env, warm up, time `steps` env steps in launches of k.  Returns (env, wall_max_s, kernel_ms per
-    env step, low_steps, gather_s, gathered)."""
+    env step, low_steps, gather_s, gathered, the timed launches' sizes)."""
     import torch
     import torch.distributed as dist
     k = k or a.k
@@ -206,6 +217,17 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             if kk < k:   # the remainder launch
                 return env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True)
             ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
+        if a.policy:   # config 5 closed loop: both levels' policies on the device (hum_hier_rollout)
+            from ilrl_amd.policy import DevicePolicy, hier_rollout
+            high = DevicePolicy.random_init_high(seed=17 + rank, device=dev.index)
+            low = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
+            acted = []   # per launch: the agent that acted per (transition, lane), counted after the timed region
+
+            def step(s, kk=k):
+                tr = hier_rollout(env, high, low, kk, explore=True, step0=s * k, trajectories=True)
+                acted.append(tr["acted"])
+                return tr
+            env._bench_acted = acted
     else:
         from ilrl_amd.clips import CLIP_NAMES
         from ilrl_amd.vec_env import HumanoidVecEnv
@@ -226,7 +248,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             def step(s, kk=1):
                 pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s, out=actbuf)
                 return env.step(actbuf, autoreset=True)
-            if k > 1:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
+            if a.fused:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
                 def step(s, kk=k):
                     return pol.rollout(env, kk, explore=True, step0=s * k, trajectories=True, fused=True)
     env.reset()
@@ -250,7 +272,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             from ilrl_amd.parallel import gather_trajectories
             got = gather_trajectories(frag, dst=0)
             if got is not None and a.dump_gather:
-                gathered.append([x.cpu() for x in got])
+                gathered.append([x[::a.dump_lane_stride].cpu() for x in got])
             gather_s += time.perf_counter() - tg
     ev1.record(stream)
     torch.cuda.synchronize(dev)
@@ -261,11 +283,14 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     kern_ms = ev0.elapsed_time(ev1) / steps   # per env step, on the launch stream (torch's current)
     wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if world > 1 else wall
     low_steps = None
-    if a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
+    if a.hier and a.policy:   # physics env-steps in the timed region: the low-level transitions the rollouts recorded
+        from ilrl_amd import _native as N
+        low_steps = float(sum(int((x == N.HUM_AGENT_LOW).sum().item()) for x in env._bench_acted[wlaunches:]))
+    elif a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
         low_steps = float(count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank))
         if world > 1:
             low_steps = _all_reduce(world, dev, a.backend, low_steps, dist.ReduceOp.SUM)   # all ranks
-    return env, wall, kern_ms, low_steps, gather_s, gathered
+    return env, wall, kern_ms, low_steps, gather_s, gathered, sizes
 
 
 def _all_reduce(world, dev, backend, x, op):
@@ -334,12 +359,12 @@ def main():
     if a.hier:
         from ilrl_amd.hier_env import HIER_CLIP
         a.clip = HIER_CLIP
-    if a.policy and not a.fused:
+    if a.policy and not a.fused and not a.hier:
         a.k = 1   # closed loop: the policy acts on every step's observation, one launch each
     if a.k < 1:
         raise SystemExit("--k must be >= 1")
-    env, wall_max, kern_ms, low_steps, gather_s, gathered = run(a, world, rank, dev, n, a.precision, a.steps, a.warmup,
-                                                                phys)
+    env, wall_max, kern_ms, low_steps, gather_s, gathered, sizes = run(a, world, rank, dev, n, a.precision, a.steps,
+                                                                       a.warmup, phys)
     flags = env.error_flags()
     if rank == 0 and a.dump_gather and gathered:
         import numpy as np
@@ -365,18 +390,21 @@ def main():
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
             "config": {"workload": ("HumanoidBulletEnv-v0-Hier two-level rollout (high heading every 5 low steps), "
                                     if a.hier else "HumanoidBulletEnv-v0-Low step+reward, ") +
-                                   "%s, %d envs/GPU, %s, auto-reset, %d env steps per launch" % (
-                                       a.clip, n, "on-GPU policy actions (random-init 70-256-256-17 tanh MLP + "
-                                       "Gaussian exploration) in the loop" if a.policy else
-                                       "uniform random actions (a fresh row per env step)", a.k),
-                       "envs_per_gpu": n, "clip": a.clip, "steps_per_launch": a.k,
+                                   "%s, %d envs/GPU, %s, auto-reset, %d env steps per %s" % (
+                                       a.clip, n, _actions_desc(a), a.k,
+                                       "hum_hier_rollout call (2 policy launches + 1 env launch per transition)"
+                                       if a.hier and a.policy else "launch"),
+                       "fused": bool(a.policy and a.fused and not a.hier),
+                       "envs_per_gpu": n, "clip": a.clip, "k": a.k,
+                       # the launches the timed region actually ran (--steps < k: one shorter launch)
+                       "launches": len(sizes), "steps_per_launch": sorted(set(sizes), reverse=True),
                        "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
             # per env step: kernel_ms = launch duration / k; achieved = the env step's algorithmic bytes over it
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "HBM bytes per env step of all lanes (PMC, profiles/pmc_traffic.json)",
                          "bytes_per_env_step": BYTES_PER_STEP_ALGO, "bytes_per_env_step_layout": BYTES_PER_STEP_LAYOUT,
-                         "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * a.k},
+                         "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * a.steps / len(sizes)},
             "error_flags": flags,
         }
         if flops:
@@ -405,7 +433,7 @@ def main():
                 runs.append(("previous_model_split_off", a.precision, dict(phys, split_penetration=-1e30), a.k))
             for name, prec, ph, kk in runs:
                 st, wu = 200, 24
-                e2, w2, k2, _, _, _ = run(a, 1, 0, dev, n, prec, st, wu, ph, k=kk)
+                e2, w2, k2, _, _, _, _ = run(a, 1, 0, dev, n, prec, st, wu, ph, k=kk)
                 e2.close()
                 sec[name] = {"value": n * st / w2, "ms_per_step": w2 / st * 1e3, "kernel_ms": k2, "steps": st,
                              "warmup": wu, "steps_per_launch": kk, "precision": prec}

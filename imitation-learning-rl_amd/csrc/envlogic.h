@@ -33,6 +33,9 @@ constexpr int EP_RIGHT_LEG = 6, EP_RIGHT_FOOT = 9;
 constexpr int PART_RIGHT_FOOT = 12;   // index of 'right_foot' in the pybullet parts order
 
 #define HUM_GLOBAL __attribute__((address_space(1)))
+// LDS, explicitly: a value read from either LDS or global memory goes through two address-space-typed loads, never
+// one load through a generic pointer (a flat access; DESIGN.md section 4, the MachineLICM fault)
+#define HUM_LDS __attribute__((address_space(3)))
 struct ClipDev {
     const double* pos; const double* vel; const double* rel; const double* ep;
     int n_pos, n_vel, n_rel, n_ep, max_frame;

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,6 +57,8 @@ struct hum_env {
     double hf_s[3], hf_o[3], hf_mid;
     void* stage;          // HUM_STEP_HOST_IO: device staging for host buffers (grown on demand)
     size_t stage_bytes;
+    void* traj;           // hum_rollout_fused without reward / done traces: their [k,n] rows (grown on demand)
+    size_t traj_bytes;
     hipGraphExec_t graph;
     int graph_k;
     const void* graph_key[6];
@@ -224,6 +227,14 @@ int hum_create(const hum_config* cfg, hum_env** out) {
         st = hipGetLastError();
         if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
     }
+    if (st == hipSuccess && getenv("ILRL_DEBUG_PTRS")) {   // diagnostics: the device buffer map (fault addresses)
+        const int epb = cfg->envs_per_block;
+        const size_t sb = (cfg->kernel == 1 ? (size_t)grow_block_size(epb, lds_rows_of(*cfg)) * ((n + epb - 1) / epb)
+                                            : (size_t)SCRATCH_PER_LANE * n) * e->real_size;
+        fprintf(stderr, "hum_create %p: phys %p +%zu bi %p +%zu bd %p +%zu scratch %p +%zu eflags %p clips %p\n", (void*)e,
+                e->d.phys, HUM_NSTATE * n * e->real_size, (void*)e->d.bi, NBOOK_I * n * sizeof(int), (void*)e->d.bd,
+                NBOOK_D * n * sizeof(double), e->d.scratch, sb, (void*)e->eflags, (void*)e->clips_dev);
+    }
     if (st != hipSuccess) {
         std::string m = std::string("hum_create: ") + hipGetErrorString(st);
         hum_destroy(e);
@@ -247,6 +258,7 @@ int hum_destroy(hum_env* e) {
     (void)hipFree(e->pred);
     (void)hipFree(e->hf);
     (void)hipFree(e->stage);
+    (void)hipFree(e->traj);
     for (int k = 0; k < HUM_MAX_CLIPS; k++) (void)hipFree(e->clip_dev[k]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -268,6 +280,8 @@ int hum_set_clip(hum_env* e, int32_t id, const double* pos, int32_t n_pos, const
     HIPCHK(hipMemcpy(buf + np + nv, rel, nr * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(buf + np + nv + nr, ep, ne * sizeof(double), hipMemcpyHostToDevice));
     e->clip_dev[id] = buf;
+    if (getenv("ILRL_DEBUG_PTRS"))
+        fprintf(stderr, "hum_set_clip %p: clip %d tables %p +%zu\n", (void*)e, id, (void*)buf, (np + nv + nr + ne) * sizeof(double));
     e->clips[id] = ClipDev{buf, buf + np, buf + np + nv, buf + np + nv + nr, n_pos, n_vel, n_rel, n_ep, n_pos - 1};
     e->clip_set[id] = true;
     HIPCHK(hipMemcpy(e->clips_dev + id, &e->clips[id], sizeof(ClipDev), hipMemcpyHostToDevice));
@@ -423,6 +437,17 @@ int staged(hum_env* e, hipStream_t s, HostBuf* bufs, int nb, F launch) {
     HIPCHK(hipStreamSynchronize(s));
     return rc;
 }
+// HUM_STEP_CHECK_FINITE, before the launch: take the non-finite-action bit out of the sticky flags on the stream, so
+// that the check after the launch reports this call's actions only (an earlier unchecked asynchronous step may have
+// left it set)
+__global__ void clear_eflag_kernel(unsigned* eflags, unsigned bits) {
+    if (threadIdx.x == 0) atomicAnd(eflags, ~bits);
+}
+int clear_nonfinite(hum_env* e, hipStream_t s) {
+    hipLaunchKernelGGL(clear_eflag_kernel, dim3(1), dim3(64), 0, s, e->eflags, (unsigned)HUM_EFLAG_NONFINITE_ACTION);
+    HIPCHK(hipGetLastError());
+    return HUM_OK;
+}
 // HUM_STEP_CHECK_FINITE: wait for the launch and turn a non-finite action (humanoid.py:55 assert) into an error
 // status; the bit is taken out of the sticky flags
 int check_finite(hum_env* e, hipStream_t s) {
@@ -465,6 +490,7 @@ int hum_step_k(hum_env* e, const float* actions, float* obs, float* reward, uint
     a.ksteps = k;
     const hipStream_t s = stream_of(e, stream);
     int rc;
+    if ((flags & HUM_STEP_CHECK_FINITE) && (rc = clear_nonfinite(e, s)) != HUM_OK) return rc;
     if (flags & HUM_STEP_HOST_IO) {
         const size_t kn = (size_t)k * e->n;
         HostBuf b[6] = {{(const void**)&a.act, kn * HUM_NACT * 4, false}, {(const void**)&a.obs, kn * HUM_NOBS * 4, true},
@@ -536,6 +562,7 @@ int hum_hier_step_k(hum_env* e, const float* high_act, const float* low_act, con
     a.ksteps = k;
     const hipStream_t s = stream_of(e, stream);
     int rc;
+    if ((flags & HUM_STEP_CHECK_FINITE) && (rc = clear_nonfinite(e, s)) != HUM_OK) return rc;
     if (flags & HUM_STEP_HOST_IO) {
         const size_t kn = (size_t)k * e->n;
         HostBuf b[12] = {{(const void**)&a.act, kn * HUM_NACT * 4, false},
@@ -812,7 +839,7 @@ int32_t hum_num_lanes(const hum_env* e) { return e ? e->n : 0; }
 }  // extern "C"
 __attribute__((visibility("hidden"))) int hum_internal_device(const hum_env* e) { return e ? e->cfg.device : -1; }
 // hum_rollout_fused (policy.hip): k sampler steps in one launch of the fused-policy cooperative kernel.  pw: the
-// hum_policy weight block.  Missing rew / done traces go to temporary buffers (the call then synchronises).
+// hum_policy weight block.  Missing rew / done traces go to the handle's scratch (grown on demand, stream-ordered).
 __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
     hum_env* e, const float* pw, uint64_t seed, int32_t k, int32_t explore, uint64_t step0, float* obs, float* obs_reset,
     uint8_t* done, float* reward, float* act_last, float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj,
@@ -827,11 +854,18 @@ __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
     const size_t kn = (size_t)k * e->n;
     float* rt = rew_traj;
     uint8_t* dt = done_traj;
-    bool tmp = false;
     if (!rt || !dt) {
-        tmp = true;
-        if (!rt) HIPCHK(hipMalloc((void**)&rt, kn * sizeof(float)));
-        if (!dt) HIPCHK(hipMalloc((void**)&dt, kn));
+        const size_t rbytes = (kn * sizeof(float) + 255) / 256 * 256, need = rbytes + kn;
+        if (need > e->traj_bytes) {   // the previous launches using it are ordered before the free on this stream
+            HIPCHK(hipStreamSynchronize(s));
+            if (e->traj) HIPCHK(hipFree(e->traj));
+            e->traj = nullptr;
+            e->traj_bytes = 0;
+            HIPCHK(hipMalloc(&e->traj, need));
+            e->traj_bytes = need;
+        }
+        if (!rt) rt = (float*)e->traj;
+        if (!dt) dt = (uint8_t*)e->traj + rbytes;
     }
     KArgs a = make_args(e);
     a.flags = HUM_STEP_AUTORESET;
@@ -860,13 +894,34 @@ __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
     if (st == hipSuccess) st = hipMemcpyAsync(reward, rt + (k - 1) * (size_t)e->n, (size_t)e->n * sizeof(float),
                                               hipMemcpyDeviceToDevice, s);
     if (st == hipSuccess) st = hipMemcpyAsync(done, dt + (k - 1) * (size_t)e->n, (size_t)e->n, hipMemcpyDeviceToDevice, s);
-    if (tmp) {
-        if (st == hipSuccess) st = hipStreamSynchronize(s);
-        if (rt != rew_traj) (void)hipFree(rt);
-        if (dt != done_traj) (void)hipFree(dt);
-    }
     if (st != hipSuccess) return fail(HUM_ERR_HIP, std::string("hum_rollout_fused: ") + hipGetErrorString(st));
     return HUM_OK;
+}
+// one hierarchical transition (hum_hier_step, agent = each lane's expected one) that also records the agent that
+// acted per lane (acted [n], may be NULL): hum_hier_rollout's env launch (policy.hip)
+__attribute__((visibility("hidden"))) int hum_internal_hier_step_acted(
+    hum_env* e, const float* high_act, const float* low_act, uint8_t* agents, float* high_obs, float* low_obs,
+    float* high_rew, float* low_rew, uint8_t* done, uint32_t flags, float* high_obs_reset, uint8_t* acted,
+    void* stream) {
+    if (!e || !high_act || !low_act || !agents || !high_obs || !low_obs || !high_rew || !low_rew || !done)
+        return fail(HUM_ERR_ARG, "hum_hier_rollout: null argument");
+    if (!e->cfg.hier) return fail(HUM_ERR_STATE, "hum_hier_rollout: handle was not created with hier = 1");
+    if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_hier_rollout: no clip uploaded (hum_set_clip)");
+    HIPCHK(hipSetDevice(e->cfg.device));
+    KArgs a = make_args(e);
+    a.act = low_act;
+    a.act_high = high_act;
+    a.agents = agents;
+    a.obs = low_obs;
+    a.obs_high = high_obs;
+    a.rew = low_rew;
+    a.rew_high = high_rew;
+    a.done = done;
+    a.flags = flags & (HUM_STEP_AUTORESET | HUM_STEP_SKIP_PHYSICS);
+    a.obs_high_reset = high_obs_reset;
+    a.acted = acted;
+    a.ksteps = 1;
+    return launch_step(e, a, stream_of(e, stream));
 }
 extern "C" {
 

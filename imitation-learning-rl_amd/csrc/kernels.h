@@ -78,6 +78,9 @@ struct KArgs {
     float* act_last;                // [n,17] the last step's clipped actions (hum_rollout's act_buf)
     unsigned long long pseed, pstep0;
     int pexplore;
+    // hierarchical env, optional [ksteps, n]: the agent that acted in each transition (HUM_AGENT_HIGH / _LOW; 0 = the
+    // lane was not stepped: no action for it, or a non-finite low-level action) - hum_hier_rollout's trajectory
+    unsigned char* acted;
 };
 
 // CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
@@ -597,9 +600,14 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
 
 // non-finite action on a lane (humanoid.py:55 assert): lane not stepped, flagged, outputs neutral
 __device__ inline void nonfinite_outputs(const KArgs& a, long io, int frame, float* obs_dst = nullptr) {
-    if (!a.hier) {
-        float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
-        for (int k = 0; k < HUM_NOBS; k++) orow[k] = 0.f;
+    if (!a.hier) {   // the LDS staging row or the global row, each through its own address space (no flat stores)
+        if (obs_dst) {
+            HUM_LDS float* orow = (HUM_LDS float*)obs_dst;
+            for (int k = 0; k < HUM_NOBS; k++) orow[k] = 0.f;
+        } else {
+            HUM_GLOBAL float* orow = (HUM_GLOBAL float*)(a.obs + io * HUM_NOBS);
+            for (int k = 0; k < HUM_NOBS; k++) orow[k] = 0.f;
+        }
     } else {
         a.rew_high[io] = 0.f;
         a.agents[io] = 0;
@@ -628,6 +636,7 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
         // no action this round (HUM_AGENT_SEL_SKIP) is left untouched and reports no agent
         if (a.hier && a.agent_sel && a.agent_sel[io] == HUM_AGENT_SEL_SKIP) {
             a.agents[io] = 0;
+            if (a.acted) a.acted[io] = 0;
             continue;
         }
         const bool high = a.hier && (a.agent_sel ? a.agent_sel[io] != 0 : b.expect_high != 0);
@@ -638,6 +647,7 @@ __global__ void __launch_bounds__(256) step_kernel(KArgs a) {
             act[k] = a.act[io * HUM_NACT + k];
             finite &= isfinite(act[k]);
         }
+        if (a.hier && a.acted) a.acted[io] = !finite && !high ? 0 : (high ? HUM_AGENT_HIGH : HUM_AGENT_LOW);
         if (!finite && !high) {   // humanoid.py:55 assert: lane not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
             nonfinite_outputs(a, io, b.frame);
@@ -684,7 +694,7 @@ __device__ inline unsigned long long pmix64(unsigned long long z) {   // policy.
 typedef float pf4 __attribute__((ext_vector_type(4)));
 // one hidden layer: F[e][dst + 4 lane + m] = tanh(sum_k F[e][src + k] W[k][4 lane + m] + B[4 lane + m])
 template <int EPB_, int K, int UNROLL>
-__device__ __attribute__((always_inline)) inline void policy_hidden(float* const (&F)[EPB_], const HUM_GLOBAL float* W,
+__device__ __attribute__((always_inline)) inline void policy_hidden(HUM_LDS float* const (&F)[EPB_], const HUM_GLOBAL float* W,
                                                                     const HUM_GLOBAL float* B, int src, int dst,
                                                                     int lane) {
     float acc[EPB_][4];
@@ -733,9 +743,9 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
     const HUM_GLOBAL float* W3 = B2 + 256;
     const HUM_GLOBAL float* B3 = W3 + 256 * HUM_NACT;
     const HUM_GLOBAL float* LSTD = B3 + HUM_NACT;
-    float* F[EPB_];
+    HUM_LDS float* F[EPB_];   // LDS-typed: no generic (flat) access
 #pragma unroll
-    for (int e = 0; e < EPB_; e++) F[e] = policy_scratch(sh[e]);
+    for (int e = 0; e < EPB_; e++) F[e] = (HUM_LDS float*)policy_scratch(sh[e]);
     // hidden layer 1 (K = 70: policy.hip's zero rows 70, 71 add exact zeros), hidden layer 2
     policy_hidden<EPB_, HUM_NOBS, 10>(F, W1, B1, PX_OFF, PH1_OFF, lane);
     wave_sync();
@@ -743,8 +753,8 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
     wave_sync();
     // output layer: chain A = (env lane / 16, column lane % 16), chain B = (env lane, column 16) in lanes < EPB_
     const int eA = lane >> 4, cA = lane & 15, eB = lane < EPB_ ? lane : 0;
-    const float* hA = F[0] + PH2_OFF;
-    const float* hB = F[0] + PH2_OFF;
+    const HUM_LDS float* hA = F[0] + PH2_OFF;
+    const HUM_LDS float* hB = F[0] + PH2_OFF;
 #pragma unroll
     for (int q = 1; q < EPB_; q++) {
         hA = eA == q ? F[q] + PH2_OFF : hA;
@@ -769,7 +779,7 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
             const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
             v = mean + expf(LSTD[c]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
         }
-        float* pa = F[0] + PACT_OFF;
+        HUM_LDS float* pa = F[0] + PACT_OFF;
 #pragma unroll
         for (int q = 1; q < EPB_; q++) pa = e == q ? F[q] + PACT_OFF : pa;
         pa[c] = fminf(fmaxf(v, -1.f), 1.f);
@@ -848,17 +858,23 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         // the sampler's input: step 0 the handle's current observation (a lane done at the previous step: its reset
         // observation), later steps the row the previous step staged (its reset row if it reset)
         float* X = policy_scratch(S) + PX_OFF;
-        const float* src = nullptr;
-        if (t == 0) {
-            if (valid) src = ((a.done_in && a.done_in[i]) ? a.obs_reset : a.obs) + (long)i * HUM_NOBS;
-        } else {
-            src = reinterpret_cast<const float*>(&S.x.aba.IA[0][0] + (prev_reset ? 144 : 72));
-        }
+        // step 0 from global memory, later steps from LDS: two address-space-typed loads (no flat access)
         float xv[5];
+        if (t == 0) {
+            const HUM_GLOBAL float* src = nullptr;
+            if (valid) src = (const HUM_GLOBAL float*)(((a.done_in && a.done_in[i]) ? a.obs_reset : a.obs) + (long)i * HUM_NOBS);
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const int k = l + GL * j;
-            xv[j] = (valid && k < HUM_NOBS) ? src[k] : 0.f;
+            for (int j = 0; j < 5; j++) {
+                const int k = l + GL * j;
+                xv[j] = (valid && k < HUM_NOBS) ? src[k] : 0.f;
+            }
+        } else {
+            const HUM_LDS float* src = (const HUM_LDS float*)reinterpret_cast<const float*>(&S.x.aba.IA[0][0] + (prev_reset ? 144 : 72));
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const int k = l + GL * j;
+                xv[j] = (valid && k < HUM_NOBS) ? src[k] : 0.f;
+            }
         }
         wave_sync();
 #pragma unroll
@@ -927,6 +943,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     Book b;
     T st[HUM_NSTATE];
     bool rst = false, booked = false;
+    if (valid && l == 0 && a.acted) a.acted[io] = skip || !env_ok ? 0 : (high ? HUM_AGENT_HIGH : HUM_AGENT_LOW);
     if (valid && l == 0 && skip) {
         a.agents[io] = 0;
     } else if (valid && l == 0) {

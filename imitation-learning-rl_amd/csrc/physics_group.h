@@ -767,11 +767,13 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             const int cidx = r < enl + enc ? r - enl : (r - enl - enc) >> 1;
             const int f = r < enl + enc ? 0 : 1 + ((r - enl - enc) & 1);
             T ce[CW];
-            if (cidx < MAXC_LDS) {
+            if (cidx < MAXC_LDS) {   // LDS and global (spilled contact) through address-space-typed pointers: the
+                                     // two loads are never merged into one flat load through a generic pointer
+                const HUM_LDS T* lc = (const HUM_LDS T*)&C.con[cidx][0];
 #pragma unroll
-                for (int k = 0; k < CW; k++) ce[k] = C.con[cidx][k];
-            } else {   // spilled contact (nontemporal: keeps the LDS path's loads ds_read, not flat)
-                const T* gc = gblock + gcon_offset(EPB_, cap, e) + (long)(cidx - MAXC_LDS) * CW;
+                for (int k = 0; k < CW; k++) ce[k] = lc[k];
+            } else {
+                const HUM_GLOBAL T* gc = (const HUM_GLOBAL T*)(gblock + gcon_offset(EPB_, cap, e) + (long)(cidx - MAXC_LDS) * CW);
 #pragma unroll
                 for (int k = 0; k < CW; k++) ce[k] = __builtin_nontemporal_load(gc + k);
             }
@@ -1590,31 +1592,37 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (; k < tmax; k += 4) round(std::true_type{}, k);
         }
     } else {
-        // the block's rows overflow its LDS pool: plain loop over pool positions (LDS or global spill region)
-        auto rowp = [&](int p) -> T* {
-            return p < cap ? reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)) : gblock + (long)(p - cap) * RW;
+        // the block's rows overflow its LDS pool: plain loop over pool positions (LDS or global spill region).  Each
+        // access is an LDS or a global one chosen per value, never one through a generic pointer that may point at
+        // either (a flat access)
+        auto rd = [&](int p, int w) -> T {
+            if (p < cap) return ((const HUM_LDS T*)((const HUM_LDS char*)shb + pool_off<T>(p)))[w];
+            return __builtin_nontemporal_load((const HUM_GLOBAL T*)(gblock + (long)(p - cap) * RW) + w);
         };
-        auto lam_of = [&](int r) -> T { return rowp(pbase + pool_pos(r, nl, nc))[RO_LAM]; };
-        auto solve = [&](T* R, int r) {
-            T lo = T(0), hi = R[RO_S0 + 1];
+        auto wr = [&](int p, int w, T v) {
+            if (p < cap) ((HUM_LDS T*)((HUM_LDS char*)shb + pool_off<T>(p)))[w] = v;
+            else __builtin_nontemporal_store(v, (HUM_GLOBAL T*)(gblock + (long)(p - cap) * RW) + w);
+        };
+        auto solve = [&](int p, int r) {
+            T lo = T(0), hi = rd(p, RO_S0 + 1);
             if (r >= nl + nc) {   // friction bounds from the normal impulse of the same contact
-                const T mu = R[RO_S1];
-                const T ln = lam_of(nl + ((r - nl - nc) >> 1));
+                const T mu = rd(p, RO_S1);
+                const T ln = rd(pbase + pool_pos(nl + ((r - nl - nc) >> 1), nl, nc), RO_LAM);
                 lo = -mu * ln;
                 hi = mu * ln;
             }
-            const T part = R[2 * l] * n0 + (l < NV - GL ? R[2 * (GL + l)] * n1 : T(0));
-            const T m0 = R[2 * l + 1], m1 = l < NV - GL ? R[2 * (GL + l) + 1] : T(0);
+            const T part = rd(p, 2 * l) * n0 + (l < NV - GL ? rd(p, 2 * (GL + l)) * n1 : T(0));
+            const T m0 = rd(p, 2 * l + 1), m1 = l < NV - GL ? rd(p, 2 * (GL + l) + 1) : T(0);
             const T jv = row_sum(part);
-            const T lam = R[RO_LAM];
-            const T lnew = clampT(lam + R[RO_S0 + 3] * (R[RO_S0] - jv), lo, hi);
+            const T lam = rd(p, RO_LAM);
+            const T lnew = clampT(lam + rd(p, RO_S0 + 3) * (rd(p, RO_S0) - jv), lo, hi);
             const T dl = lnew - lam;
-            R[RO_LAM] = lnew;
+            wr(p, RO_LAM, lnew);
             n0 += m0 * dl;
             n1 += m1 * dl;
         };
         for (int it = 0; it < P.iters; it++)
-            for (int r = 0; r < nrows; r++) solve(rowp(pbase + pool_pos(r, nl, nc)), r);
+            for (int r = 0; r < nrows; r++) solve(pbase + pool_pos(r, nl, nc), r);
     }
     PHASE(8);
     S.nu[l] = n0;

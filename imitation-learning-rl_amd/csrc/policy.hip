@@ -4,7 +4,9 @@
 // Network (train_config.py:107-111, RLlib 1.2 FullyConnectedNetwork with fcnet_hiddens [256, 256],
 // fcnet_activation tanh, free_log_std True): mean = W3 tanh(W2 tanh(W1 obs + b1) + b2) + b3, action distribution
 // DiagGaussian(mean, exp(log_std)); RLlib's clip_actions clips the sample to the Box [-1, 1] before env.step.
-// Weights are fp32 [in][out] (the TF kernel layout RLlib's get_weights() returns).
+// Weights are fp32 [in][out] (the TF kernel layout RLlib's get_weights() returns).  Two shapes are in use: the
+// low-level policy 70 -> 17 and the hierarchical env's high-level policy 44 -> 2 (train_config.py:23-27, 262-298:
+// the same FCNet on the 44-dim high observation and the 2-dim heading action); any n_in <= 72, n_out <= 32 works.
 //
 // MI355X mapping: one block = 16 envs x 16 waves (1024 threads; 4096 envs = 256 blocks = one per CU, four waves
 // per SIMD).  Wave w owns the 16x16 output tile of columns 16w..16w+15 of each hidden layer (waves 0, 1 the two
@@ -26,10 +28,14 @@ int hum_internal_device(const hum_env* env);   // humanoid_env.hip
 int hum_internal_rollout_fused(hum_env* e, const float* pw, uint64_t seed, int32_t k, int32_t explore, uint64_t step0,
                                float* obs, float* obs_reset, uint8_t* done, float* reward, float* act_last,
                                float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj, void* stream);
+int hum_internal_hier_step_acted(hum_env* e, const float* high_act, const float* low_act, uint8_t* agents,
+                                 float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done,
+                                 uint32_t flags, float* high_obs_reset, uint8_t* acted, void* stream);
 
 namespace {
 
-constexpr int OBS = HUM_NOBS, ACT = HUM_NACT, H = 256, K1 = 72;   // K1: 70 padded to a multiple of 4
+constexpr int H = 256, K1 = 72;   // K1: the largest input (70) padded to a multiple of 4; inputs n_in <= K1
+constexpr int MAX_OUT = 32;         // outputs n_out <= two 16-wide tiles
 constexpr int ROWS = 16, WAVES = H / 16;
 // B-fragment layout: [tile][k-step quad][lane][4]; k-steps per layer 18 (K1 / 4, quads padded to 5), 64, 64
 constexpr int SQ1 = 5, SQ2 = 16, SQ3 = 16, NT3 = 2;
@@ -42,7 +48,7 @@ struct PolicyArgs {
     const float* log_std;
     const float* obs; const float* obs_reset; const unsigned char* done;
     float* act; float* mean_out; float* obs_in_out; float* raw_out;
-    int n, explore;
+    int n, explore, n_in, n_out;
     unsigned long long seed, step;
 };
 
@@ -102,12 +108,12 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
     for (int e = tid; e < ROWS * K1; e += blockDim.x) {
         const int r = e / K1, k = e - r * K1, i = row0 + r;
         float v = 0.f;
-        if (i < p.n && k < OBS) {
+        if (i < p.n && k < p.n_in) {
             const bool rs = p.obs_reset && p.done && p.done[i];
-            v = (rs ? p.obs_reset : p.obs)[(long)i * OBS + k];
+            v = (rs ? p.obs_reset : p.obs)[(long)i * p.n_in + k];
         }
         xs[r * PX + k] = v;
-        if (p.obs_in_out && i < p.n && k < OBS) p.obs_in_out[(long)i * OBS + k] = v;
+        if (p.obs_in_out && i < p.n && k < p.n_in) p.obs_in_out[(long)i * p.n_in + k] = v;
     }
     __syncthreads();
     const int c = 16 * wave + (l & 15);   // C/D map: lane l, register q -> row 4 (l >> 4) + q, column l & 15
@@ -125,14 +131,14 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
         for (int q = 0; q < 4; q++) h2[(4 * (l >> 4) + q) * PH + c] = tanhf(acc[q] + bias);
     }
     __syncthreads();
-    if (wave < NT3) {   // output layer: 17 columns = two 16-wide tiles, one per wave
+    if (wave < NT3 && 16 * wave < p.n_out) {   // output layer: up to two 16-wide tiles of columns, one per wave
         f32x4 b3f[SQ3];
         load_frags<SQ3>(p.f3, wave, b3f);
         const f32x4 o = mfma_tile<H / 4>(h2, PH, b3f);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int r = 4 * (l >> 4) + q, c3 = 16 * wave + (l & 15), i = row0 + r;
-            if (c3 < ACT && i < p.n) {
+            if (c3 < p.n_out && i < p.n) {
                 const float mean = o[q] + p.b3[c3];
                 float a = mean;
                 if (p.explore) {   // DiagGaussian sample: mean + exp(log_std) * N(0, 1), counter-based Box-Muller
@@ -142,9 +148,10 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
                     const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
                     a = mean + expf(p.log_std[c3]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
                 }
-                p.act[(long)i * ACT + c3] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
-                if (p.raw_out) p.raw_out[(long)i * ACT + c3] = a;           // the sample itself (SampleBatch actions)
-                if (p.mean_out) p.mean_out[(long)i * ACT + c3] = mean;
+                const long o = (long)i * p.n_out + c3;
+                p.act[o] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
+                if (p.raw_out) p.raw_out[o] = a;           // the sample itself (SampleBatch actions)
+                if (p.mean_out) p.mean_out[o] = mean;
             }
         }
     }
@@ -154,6 +161,7 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
 
 struct hum_policy {
     int device;
+    int n_in, n_out;
     float* w;   // one allocation: w1 b1 w2 b2 w3 b3 log_std, then the B fragments of w1, w2, w3
     const float *w1, *b1, *w2, *b2, *w3, *b3, *log_std, *f1, *f2, *f3;
     unsigned long long seed;
@@ -170,31 +178,42 @@ extern "C" {
 
 int hum_policy_create(int32_t device, const float* w1, const float* b1, const float* w2, const float* b2,
                       const float* w3, const float* b3, const float* log_std, uint64_t seed, hum_policy** out) {
+    return hum_policy_create_ex(device, HUM_NOBS, HUM_NACT, w1, b1, w2, b2, w3, b3, log_std, seed, out);
+}
+
+int hum_policy_create_ex(int32_t device, int32_t n_in, int32_t n_out, const float* w1, const float* b1, const float* w2,
+                         const float* b2, const float* w3, const float* b3, const float* log_std, uint64_t seed,
+                         hum_policy** out) {
     if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !out) return perr(HUM_ERR_ARG, "hum_policy_create: null argument");
+    if (n_in < 1 || n_in > K1 || n_out < 1 || n_out > MAX_OUT)
+        return perr(HUM_ERR_ARG, "hum_policy_create: n_in must be in [1, 72] and n_out in [1, 32]");
     if (hipSetDevice(device) != hipSuccess) return perr(HUM_ERR_HIP, "hum_policy_create: hipSetDevice");
-    // w1 is stored padded to K1 rows (rows 70, 71 zero) so the kernel's k loop needs no bound
-    const size_t n1 = (size_t)K1 * H, n2 = (size_t)H * H, n3 = (size_t)H * ACT;
-    const size_t nw = (n1 + H + n2 + H + n3 + ACT + ACT + 63) / 64 * 64;   // fragments 16-byte aligned
+    // w1 is stored padded to K1 rows (rows n_in .. 71 zero) so the kernel's k loop needs no bound; the block layout
+    // (w1 [72][256], b1, w2, b2, w3 [256][n_out], b3, log_std) is what hum_rollout_fused's in-kernel network reads
+    const size_t n1 = (size_t)K1 * H, n2 = (size_t)H * H, n3 = (size_t)H * n_out;
+    const size_t nw = (n1 + H + n2 + H + n3 + n_out + n_out + 63) / 64 * 64;   // fragments 16-byte aligned
     const size_t total = nw + FRAG1 + FRAG2 + FRAG3;
     hum_policy* p = new hum_policy();
     p->device = device;
+    p->n_in = n_in;
+    p->n_out = n_out;
     p->seed = seed;
     if (hipMalloc((void**)&p->w, total * sizeof(float)) != hipSuccess) {
         delete p;
         return perr(HUM_ERR_HIP, "hum_policy_create: hipMalloc");
     }
     float* h = new float[total]();
-    std::memcpy(h, w1, (size_t)OBS * H * sizeof(float));
+    std::memcpy(h, w1, (size_t)n_in * H * sizeof(float));
     size_t o = n1;
     std::memcpy(h + o, b1, H * sizeof(float)); o += H;
     std::memcpy(h + o, w2, n2 * sizeof(float)); o += n2;
     std::memcpy(h + o, b2, H * sizeof(float)); o += H;
     std::memcpy(h + o, w3, n3 * sizeof(float)); o += n3;
-    std::memcpy(h + o, b3, ACT * sizeof(float)); o += ACT;
-    if (log_std) std::memcpy(h + o, log_std, ACT * sizeof(float));
-    frag_layout(w1, OBS, H, H, WAVES, SQ1, h + nw);
+    std::memcpy(h + o, b3, n_out * sizeof(float)); o += n_out;
+    if (log_std) std::memcpy(h + o, log_std, n_out * sizeof(float));
+    frag_layout(w1, n_in, H, H, WAVES, SQ1, h + nw);
     frag_layout(w2, H, H, H, WAVES, SQ2, h + nw + FRAG1);
-    frag_layout(w3, H, ACT, ACT, NT3, SQ3, h + nw + FRAG1 + FRAG2);
+    frag_layout(w3, H, n_out, n_out, NT3, SQ3, h + nw + FRAG1 + FRAG2);
     const hipError_t st = hipMemcpy(p->w, h, total * sizeof(float), hipMemcpyHostToDevice);
     delete[] h;
     if (st != hipSuccess) {
@@ -203,7 +222,7 @@ int hum_policy_create(int32_t device, const float* w1, const float* b1, const fl
         return perr(HUM_ERR_HIP, "hum_policy_create: hipMemcpy");
     }
     p->w1 = p->w; p->b1 = p->w1 + n1; p->w2 = p->b1 + H; p->b2 = p->w2 + n2; p->w3 = p->b2 + H;
-    p->b3 = p->w3 + n3; p->log_std = p->b3 + ACT;
+    p->b3 = p->w3 + n3; p->log_std = p->b3 + n_out;
     p->f1 = p->w + nw; p->f2 = p->f1 + FRAG1; p->f3 = p->f2 + FRAG2;
     *out = p;
     return HUM_OK;
@@ -233,7 +252,7 @@ int hum_policy_act_ex(hum_policy* p, const float* obs, const float* obs_reset, c
     a.w1 = p->w1; a.b1 = p->b1; a.w2 = p->w2; a.b2 = p->b2; a.w3 = p->w3; a.b3 = p->b3; a.log_std = p->log_std;
     a.obs = obs; a.obs_reset = obs_reset; a.done = done; a.act = actions; a.mean_out = mean_out; a.obs_in_out = obs_in_out;
     a.raw_out = raw_out;
-    a.n = n; a.explore = explore; a.seed = p->seed; a.step = step;
+    a.n = n; a.explore = explore; a.seed = p->seed; a.step = step; a.n_in = p->n_in; a.n_out = p->n_out;
     hipLaunchKernelGGL(policy_kernel, dim3((n + ROWS - 1) / ROWS), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
     const hipError_t st = hipGetLastError();
     if (st != hipSuccess) return perr(HUM_ERR_HIP, std::string("hum_policy_act: ") + hipGetErrorString(st));
@@ -252,6 +271,8 @@ int hum_rollout(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_
                 uint8_t* done_traj, void* stream) {
     if (!env || !p || k <= 0 || !obs || !obs_reset || !done || !reward || !act_buf)
         return perr(HUM_ERR_ARG, "hum_rollout: bad argument");
+    if (p->n_in != HUM_NOBS || p->n_out != HUM_NACT)
+        return perr(HUM_ERR_ARG, "hum_rollout: the policy must map the 70-dim observation to the 17 actions");
     if (hum_internal_device(env) != p->device)
         return perr(HUM_ERR_ARG, "hum_rollout: the env handle and the policy are on different devices");
     const int n = hum_num_lanes(env);
@@ -278,10 +299,60 @@ int hum_rollout_fused(hum_env* env, hum_policy* p, int32_t k, int32_t explore, u
                       float* rew_traj, uint8_t* done_traj, void* stream) {
     if (!env || !p || k <= 0 || !obs || !obs_reset || !done || !reward || !act_buf)
         return perr(HUM_ERR_ARG, "hum_rollout_fused: bad argument");
+    if (p->n_in != HUM_NOBS || p->n_out != HUM_NACT)
+        return perr(HUM_ERR_ARG, "hum_rollout_fused: the policy must map the 70-dim observation to the 17 actions");
     if (hum_internal_device(env) != p->device)
         return perr(HUM_ERR_ARG, "hum_rollout_fused: the env handle and the policy are on different devices");
     return hum_internal_rollout_fused(env, p->w, p->seed, k, explore, step0, obs, obs_reset, done, reward, act_buf,
                                       obs_traj, act_traj, rew_traj, done_traj, stream);
+}
+
+int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
+                     const hum_hier_io* io, const hum_hier_traj* tr, void* stream) {
+    if (!env || !high || !low || k <= 0 || !io) return perr(HUM_ERR_ARG, "hum_hier_rollout: bad argument");
+    if (!io->obs_high || !io->obs_high_reset || !io->obs_low || !io->done || !io->agents || !io->rew_high ||
+        !io->rew_low || !io->act_high || !io->act_low)
+        return perr(HUM_ERR_ARG, "hum_hier_rollout: every hum_hier_io buffer is required");
+    if (high->n_in != HUM_NOBS_HIGH || high->n_out != HUM_NACT_HIGH || low->n_in != HUM_NOBS || low->n_out != HUM_NACT)
+        return perr(HUM_ERR_ARG, "hum_hier_rollout: needs a (44, 2) high-level and a (70, 17) low-level policy");
+    if (hum_internal_device(env) != high->device || hum_internal_device(env) != low->device)
+        return perr(HUM_ERR_ARG, "hum_hier_rollout: the env handle and the policies are on different devices");
+    const hum_hier_traj none = {};
+    const hum_hier_traj& T = tr ? *tr : none;
+    const size_t n = (size_t)hum_num_lanes(env);
+    hipStream_t s = (hipStream_t)stream;
+    // per transition: the step's agents / rewards / done go straight into the trajectory rows when recorded (every
+    // lane's are written when the agent is each lane's expected one), and the next transition reads done from there
+    const uint8_t* done_prev = io->done;
+    for (int t = 0; t < k; t++) {
+        const size_t r = (size_t)t * n;
+        int rc = hum_policy_act_ex(high, io->obs_high, io->obs_high_reset, done_prev, (int32_t)n, io->act_high, nullptr,
+                                   T.obs_high ? T.obs_high + r * HUM_NOBS_HIGH : nullptr,
+                                   T.act_high ? T.act_high + r * HUM_NACT_HIGH : nullptr, explore, step0 + (uint64_t)t,
+                                   stream);
+        if (rc != HUM_OK) return rc;
+        rc = hum_policy_act_ex(low, io->obs_low, nullptr, nullptr, (int32_t)n, io->act_low, nullptr,
+                               T.obs_low ? T.obs_low + r * HUM_NOBS : nullptr,
+                               T.act_low ? T.act_low + r * HUM_NACT : nullptr, explore, step0 + (uint64_t)t, stream);
+        if (rc != HUM_OK) return rc;
+        uint8_t* ag = T.agents ? T.agents + r : io->agents;
+        float* rh = T.rew_high ? T.rew_high + r : io->rew_high;
+        float* rl = T.rew_low ? T.rew_low + r : io->rew_low;
+        uint8_t* dn = T.done ? T.done + r : io->done;
+        rc = hum_internal_hier_step_acted(env, io->act_high, io->act_low, ag, io->obs_high, io->obs_low, rh, rl, dn,
+                                          HUM_STEP_AUTORESET, io->obs_high_reset, T.acted ? T.acted + r : nullptr, stream);
+        if (rc != HUM_OK) return rc;
+        done_prev = dn;
+    }
+    // the last transition's rows into the env buffers (when they went to the trajectory)
+    const size_t last = (size_t)(k - 1) * n;
+    struct { void* dst; const void* src; size_t bytes; } cp[4] = {
+        {io->agents, T.agents ? T.agents + last : nullptr, n}, {io->rew_high, T.rew_high ? T.rew_high + last : nullptr, 4 * n},
+        {io->rew_low, T.rew_low ? T.rew_low + last : nullptr, 4 * n}, {io->done, T.done ? T.done + last : nullptr, n}};
+    for (auto& c : cp)
+        if (c.src && hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return perr(HUM_ERR_HIP, "hum_hier_rollout: copy of the last transition's rows");
+    return HUM_OK;
 }
 
 }  // extern "C"

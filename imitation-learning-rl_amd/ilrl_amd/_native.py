@@ -8,8 +8,14 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB_PATH = os.path.join(HERE, "_lib", "libhumenv.so")
 LIB_PATH = os.environ.get("ILRL_AMD_LIB", DEFAULT_LIB_PATH)
+# ILRL_AMD_AB=1 (same-box A/B runs against an older build named by ILRL_AMD_LIB): entry points the older library
+# lacks stay unbound placeholders, and its ABI may be any of AB_COMPATIBLE_ABIS (ABIs whose structs and existing
+# signatures are unchanged - later ones only added entry points).  Without it every library, override or not,
+# must match HUM_ABI_VERSION and export every symbol.
+AB_MODE = os.environ.get("ILRL_AMD_AB") == "1"
+AB_COMPATIBLE_ABIS = (8, 9)   # ABI 10 added hum_policy_create_ex, hum_hier_rollout
 
-HUM_ABI_VERSION = 9   # include/humanoid_env.h
+HUM_ABI_VERSION = 10   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
@@ -43,7 +49,8 @@ EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_creat
            "hum_get_error_flags", "hum_sync", "hum_num_lanes", "hum_stream", "hum_hier_reset", "hum_hier_step",
            "hum_reset_ex", "hum_hier_reset_ex", "hum_clip_csv_sizes", "hum_clip_csv_parse", "hum_load_clip_csv",
            "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout", "hum_rollout_fused", "hum_set_terrain",
-           "hum_step_k", "hum_hier_step_k", "hum_set_terrain_ex", "hum_policy_act_ex"]
+           "hum_step_k", "hum_hier_step_k", "hum_set_terrain_ex", "hum_policy_act_ex", "hum_policy_create_ex",
+           "hum_hier_rollout"]
 
 
 class HumConfig(ctypes.Structure):
@@ -58,6 +65,16 @@ class HumConfig(ctypes.Structure):
                 ("joint_damping", ctypes.c_int32), ("kernel", ctypes.c_int32),
                 ("hier", ctypes.c_int32), ("envs_per_block", ctypes.c_int32), ("lds_rows", ctypes.c_int32),
                 ("numpy_semantics", ctypes.c_int32), ("split_penetration", ctypes.c_double)]
+
+
+class HumHierIO(ctypes.Structure):   # hum_hier_io
+    _fields_ = [(k, ctypes.c_void_p) for k in ("obs_high", "obs_high_reset", "obs_low", "done", "agents", "rew_high",
+                                               "rew_low", "act_high", "act_low")]
+
+
+class HumHierTraj(ctypes.Structure):   # hum_hier_traj
+    _fields_ = [(k, ctypes.c_void_p) for k in ("acted", "obs_high", "act_high", "obs_low", "act_low", "agents",
+                                               "rew_high", "rew_low", "done")]
 
 
 class NativeError(RuntimeError):
@@ -76,9 +93,13 @@ def lib():
         raise NativeError("HIP library %s not found: build it with `make -C imitation-learning-rl_amd/csrc` "
                           "or __graft_entry__.build()" % LIB_PATH)
     L = ctypes.CDLL(LIB_PATH)
-    if LIB_PATH != DEFAULT_LIB_PATH:
-        # a diagnostic override (ILRL_AMD_LIB: an older build in a same-box A/B) may predate later entry points;
-        # they stay unbound placeholders there (tests/test_cpu_abi_model.py checks the shipped library has them all)
+    if AB_MODE:
+        # an older build in a same-box A/B may predate later entry points; they stay unbound placeholders there
+        # (tests/test_cpu_abi_model.py checks the shipped library has them all)
+        L.hum_abi_version.restype = ctypes.c_int
+        if L.hum_abi_version() not in AB_COMPATIBLE_ABIS + (HUM_ABI_VERSION,):
+            raise NativeError("ILRL_AMD_AB: %s has ABI %d, not one of %s" % (LIB_PATH, L.hum_abi_version(),
+                                                                           AB_COMPATIBLE_ABIS + (HUM_ABI_VERSION,)))
         import types
         for name in EXPORTS:
             if not hasattr(L, name):
@@ -103,6 +124,8 @@ def lib():
     L.hum_clip_csv_parse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, dp, dp, dp, dp]
     L.hum_load_clip_csv.argtypes = [vp, i32, ctypes.c_char_p, ctypes.c_char_p]
     L.hum_policy_create.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(vp)]
+    L.hum_policy_create_ex.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(vp)]
+    L.hum_hier_rollout.argtypes = [vp, vp, vp, i32, i32, u64, ctypes.POINTER(HumHierIO), ctypes.POINTER(HumHierTraj), vp]
     L.hum_policy_destroy.argtypes = [vp]
     L.hum_policy_act.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, u64, vp]
     L.hum_policy_act_ex.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, i32, u64, vp]
@@ -127,9 +150,9 @@ def lib():
     L.hum_stream.restype = vp
     for name in EXPORTS:
         getattr(L, name)  # AttributeError if the library lacks a declared symbol
-    if L.hum_abi_version() != HUM_ABI_VERSION and LIB_PATH == DEFAULT_LIB_PATH:   # (an A/B override may be older)
-        raise NativeError("libhumenv.so ABI %d != binding ABI %d: rebuild the library"
-                          % (L.hum_abi_version(), HUM_ABI_VERSION))
+    if L.hum_abi_version() != HUM_ABI_VERSION and not AB_MODE:
+        raise NativeError("%s: ABI %d != binding ABI %d: rebuild the library"
+                          % (LIB_PATH, L.hum_abi_version(), HUM_ABI_VERSION))
     if hasattr(L, "hum_debug_phase_cycles"):   # diagnostic builds only
         L.hum_debug_phase_cycles.argtypes = [vp, ctypes.c_int]
     _lib = L

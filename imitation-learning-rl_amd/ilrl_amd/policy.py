@@ -1,11 +1,14 @@
-"""On-GPU policy inference and a device-resident sampler loop over the C-ABI
-(include/humanoid_env.h: hum_policy_create / hum_policy_act / hum_rollout).
+"""On-GPU policy inference and device-resident sampler loops over the C-ABI
+(include/humanoid_env.h: hum_policy_create_ex / hum_policy_act / hum_rollout / hum_rollout_fused /
+hum_hier_rollout).
 
 The network is the reference's PPO policy (train_config.py:107-111: RLlib 1.2 FullyConnectedNetwork,
 fcnet_hiddens [256, 256], fcnet_activation tanh, free_log_std True): action mean =
 W3 tanh(W2 tanh(W1 obs + b1) + b2) + b3, sampled as DiagGaussian(mean, exp(log_std)) and clipped to the
 action Box (RLlib clip_actions).  Weights come from `from_rllib_weights` (the dict a TF policy's
 get_weights() returns, exported where Ray runs) or `random_init` (RLlib's normc initialisers; benchmarks).
+Two shapes: the low-level policy 70 -> 17 and the hierarchical env's high-level policy 44 -> 2 (train_config.py:
+23-27, 262-298), which `hier_rollout` drives together on a HierVecEnv (BASELINE config 5).
 The reference's trained checkpoints are pickles that the safe loaders refuse, so no
 trained weights ship here.
 """
@@ -29,16 +32,18 @@ def _normc(rng, shape, std):
 
 
 class DevicePolicy:
-    """The policy network on one GPU (weights fp32, TF kernel layout [in][out])."""
+    """The policy network on one GPU (weights fp32, TF kernel layout [in][out]); n_in -> n_out = 70 -> 17 (the
+    low-level policy) or 44 -> 2 (the high-level one)."""
 
     KEYS = ("w1", "b1", "w2", "b2", "w3", "b3", "log_std")
 
-    def __init__(self, weights, device=0, seed=0):
+    def __init__(self, weights, device=0, seed=0, n_in=N.HUM_NOBS, n_out=N.HUM_NACT):
         import torch
         self.torch = torch
         self.device = torch.device("cuda", device)
-        shapes = {"w1": (N.HUM_NOBS, H), "b1": (H,), "w2": (H, H), "b2": (H,), "w3": (H, N.HUM_NACT),
-                  "b3": (N.HUM_NACT,), "log_std": (N.HUM_NACT,)}
+        self.n_in, self.n_out = n_in, n_out
+        shapes = {"w1": (n_in, H), "b1": (H,), "w2": (H, H), "b2": (H,), "w3": (H, n_out),
+                  "b3": (n_out,), "log_std": (n_out,)}
         self.w = {}
         for k in self.KEYS:
             a = np.ascontiguousarray(weights.get(k, np.zeros(shapes[k])), dtype=np.float32)
@@ -46,20 +51,25 @@ class DevicePolicy:
                 raise ValueError("%s: shape %s, expected %s" % (k, a.shape, shapes[k]))
             self.w[k] = a
         h = ctypes.c_void_p()
-        N.check(N.lib().hum_policy_create(device, *[_fp(self.w[k]) for k in self.KEYS], ctypes.c_uint64(seed),
-                                          ctypes.byref(h)), "hum_policy_create")
+        N.check(N.lib().hum_policy_create_ex(device, n_in, n_out, *[_fp(self.w[k]) for k in self.KEYS],
+                                             ctypes.c_uint64(seed), ctypes.byref(h)), "hum_policy_create")
         self.h = h
 
     @classmethod
-    def random_init(cls, seed=0, device=0, log_std=-0.5):
+    def random_init(cls, seed=0, device=0, log_std=-0.5, n_in=N.HUM_NOBS, n_out=N.HUM_NACT):
         rng = np.random.default_rng(seed)
-        w = {"w1": _normc(rng, (N.HUM_NOBS, H), 1.0), "b1": np.zeros(H), "w2": _normc(rng, (H, H), 1.0),
-             "b2": np.zeros(H), "w3": _normc(rng, (H, N.HUM_NACT), 0.01), "b3": np.zeros(N.HUM_NACT),
-             "log_std": np.full(N.HUM_NACT, log_std)}
-        return cls(w, device=device, seed=seed)
+        w = {"w1": _normc(rng, (n_in, H), 1.0), "b1": np.zeros(H), "w2": _normc(rng, (H, H), 1.0),
+             "b2": np.zeros(H), "w3": _normc(rng, (H, n_out), 0.01), "b3": np.zeros(n_out),
+             "log_std": np.full(n_out, log_std)}
+        return cls(w, device=device, seed=seed, n_in=n_in, n_out=n_out)
 
     @classmethod
-    def from_rllib_weights(cls, weights, device=0, seed=0):
+    def random_init_high(cls, seed=0, device=0, log_std=-0.5):
+        """The hierarchical env's high-level policy shape (44 -> 2)."""
+        return cls.random_init(seed=seed, device=device, log_std=log_std, n_in=N.HUM_NOBS_HIGH, n_out=N.HUM_NACT_HIGH)
+
+    @classmethod
+    def from_rllib_weights(cls, weights, device=0, seed=0, n_in=N.HUM_NOBS, n_out=N.HUM_NACT):
         """From a TF FullyConnectedNetwork's get_weights() dict (variable name -> array): the policy branch
         fc_1, fc_2, fc_out and the free log_std variable (value-branch variables are ignored).  The name mapping
         follows RLlib 1.2's naming; it is not exercised against a real checkpoint here (no Ray in this image)."""
@@ -71,7 +81,7 @@ class DevicePolicy:
         w = {"w1": pick("fc_1/kernel"), "b1": pick("fc_1/bias"), "w2": pick("fc_2/kernel"), "b2": pick("fc_2/bias"),
              "w3": pick("fc_out/kernel"), "b3": pick("fc_out/bias"), "log_std": pick("log_std")}
         w["log_std"] = w["log_std"].reshape(-1)
-        return cls(w, device=device, seed=seed)
+        return cls(w, device=device, seed=seed, n_in=n_in, n_out=n_out)
 
     def close(self):
         if getattr(self, "h", None):
@@ -88,11 +98,13 @@ class DevicePolicy:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     def act(self, obs, obs_reset=None, done=None, explore=False, step=0, out=None, mean_out=None, raw_out=None):
-        """actions [n,17] (device, clipped to the Box) for device observations obs [n,70] (done lanes read
+        """actions [n,n_out] (device, clipped to the Box) for device observations obs [n,n_in] (done lanes read
         obs_reset); raw_out receives the samples before clip_actions (RLlib's SampleBatch actions)."""
         t = self.torch
         n = obs.shape[0]
-        act = out if out is not None else t.empty(n, N.HUM_NACT, dtype=t.float32, device=self.device)
+        if obs.shape[1] != self.n_in:
+            raise ValueError("obs must be [n, %d], got %s" % (self.n_in, tuple(obs.shape)))
+        act = out if out is not None else t.empty(n, self.n_out, dtype=t.float32, device=self.device)
         p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
         N.check(N.lib().hum_policy_act_ex(self.h, p(obs), p(obs_reset), p(done), n, p(act), p(mean_out), None,
                                           p(raw_out), int(bool(explore)), ctypes.c_uint64(step), self._stream()),
@@ -122,6 +134,38 @@ class DevicePolicy:
                    p(tr.get("obs")), p(tr.get("actions")), p(tr.get("rewards")), p(tr.get("dones")),
                    venv._stream()), "hum_rollout_fused" if fused else "hum_rollout")
         return tr
+
+
+def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True):
+    """k transitions of the two-level env venv (a HierVecEnv after reset()) with the high-level policy `high`
+    (44 -> 2) and the low-level policy `low` (70 -> 17), all on the device (hum_hier_rollout): per transition each
+    lane steps with the action of the agent it expects.  venv's buffers carry the state between calls (obs_high /
+    obs_high_reset / obs / done / agents / rewards).  Returns the trajectory {acted [k,n] (HUM_AGENT_HIGH / _LOW),
+    obs_high [k,n,44], act_high [k,n,2], obs_low [k,n,70], act_low [k,n,17] (raw samples), agents [k,n],
+    rew_high [k,n], rew_low [k,n], done [k,n]} (or {})."""
+    import torch as t
+    n, dev = venv.n, venv.device
+    if not hasattr(venv, "_act_high_buf"):
+        venv._act_high_buf = t.zeros(n, N.HUM_NACT_HIGH, dtype=t.float32, device=dev)
+        venv._act_low_buf = t.zeros(n, N.HUM_NACT, dtype=t.float32, device=dev)
+    tr = {}
+    if trajectories:
+        f32, u8 = t.float32, t.uint8
+        tr = {"acted": t.empty(k, n, dtype=u8, device=dev),
+              "obs_high": t.empty(k, n, N.HUM_NOBS_HIGH, dtype=f32, device=dev),
+              "act_high": t.empty(k, n, N.HUM_NACT_HIGH, dtype=f32, device=dev),
+              "obs_low": t.empty(k, n, N.HUM_NOBS, dtype=f32, device=dev),
+              "act_low": t.empty(k, n, N.HUM_NACT, dtype=f32, device=dev),
+              "agents": t.empty(k, n, dtype=u8, device=dev), "rew_high": t.empty(k, n, dtype=f32, device=dev),
+              "rew_low": t.empty(k, n, dtype=f32, device=dev), "done": t.empty(k, n, dtype=u8, device=dev)}
+    p = lambda x: x.data_ptr() if x is not None else None
+    io = N.HumHierIO(p(venv.obs_high), p(venv.obs_high_reset), p(venv.obs), p(venv.done), p(venv.agents),
+                     p(venv.reward_high), p(venv.reward), p(venv._act_high_buf), p(venv._act_low_buf))
+    traj = N.HumHierTraj(*[p(tr.get(f)) for f, _ in N.HumHierTraj._fields_]) if trajectories else None
+    N.check(N.lib().hum_hier_rollout(venv.h, high.h, low.h, k, int(bool(explore)), ctypes.c_uint64(step0),
+                                     ctypes.byref(io), ctypes.byref(traj) if traj is not None else None,
+                                     venv._stream()), "hum_hier_rollout")
+    return tr
 
 
 def reference_mean(w, obs):

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 9
+#define HUM_ABI_VERSION 10
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -300,6 +300,14 @@ int hum_hier_step_k(hum_env* env, const float* high_act, const float* low_act, c
 typedef struct hum_policy hum_policy;
 int hum_policy_create(int32_t device, const float* w1, const float* b1, const float* w2, const float* b2,
                       const float* w3, const float* b3, const float* log_std, uint64_t seed, hum_policy** out);
+/* The same network for any input / output width n_in <= 72, n_out <= 32: w1 [n_in,256], w3 [256,n_out], b3 and
+ * log_std [n_out]; the observation and action rows of hum_policy_act are then n_in / n_out wide.  The hierarchical
+ * env's high-level policy is 44 -> 2 (train_config.py:23-27, 262-298: "high_level_policy" on the 44-dim high
+ * observation, 2-dim heading action, same FCNet config); hum_policy_create is (70, 17).  hum_rollout and
+ * hum_rollout_fused need a (70, 17) policy. */
+int hum_policy_create_ex(int32_t device, int32_t n_in, int32_t n_out, const float* w1, const float* b1, const float* w2,
+                         const float* b2, const float* w3, const float* b3, const float* log_std, uint64_t seed,
+                         hum_policy** out);
 int hum_policy_destroy(hum_policy* policy);
 /* actions [n,17] (device) = clip(mean + explore * exp(log_std) * N(0,1), -1, 1) (RLlib clip_actions) for the
  * observations obs [n,70]; lanes with done[i] != 0 read obs_reset[i] instead (the auto-reset observation; both
@@ -324,13 +332,53 @@ int hum_rollout(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, ui
 /* hum_rollout in ONE launch: the policy network is evaluated inside the multi-step env kernel (per wave, before
  * each step's physics), so the k steps keep their state in LDS and the launch's slowest-wave tail is paid once per k
  * steps instead of once per step.  Same arguments and outputs as hum_rollout (act_buf receives the last step's
- * clipped actions; obs / obs_reset / done / reward end as the last step left them).  The policy arithmetic is the
+ * clipped actions; obs / done / reward end as the last step left them) with one difference: obs_reset receives
+ * the reset observation of the lanes done at the LAST step only (hum_rollout writes it at every step's resets;
+ * inside the launch a reset lane's new observation goes straight to the next step's policy and into obs_traj).
+ * Without rew_traj / done_traj the per-step rows go to scratch kept on the handle (grown on demand, no sync).  The policy arithmetic is the
  * same k-ordered fp32 fma chains; the physics is the benchmarked kernel's.  Needs a handle with the cooperative fp32
  * kernel, 4 envs per block, plane ground and the low-level env (HUM_ERR_STATE otherwise: use hum_rollout).
  * Replaces: the RLlib sampler's compute_actions -> env.step loop (train_config.py:107-111, low_level_env.py:475). */
 int hum_rollout_fused(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
                       float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
                       float* rew_traj, uint8_t* done_traj, void* stream);
+
+/* ---- Two-level sampler loop (BASELINE config 5; hier_env.py:355-366, 538-642 driven by the reference's two PPO
+ * policies, train_config.py:262-298 policy_mapping_fn: "high_level_agent" -> high_level_policy (44 -> 2),
+ * "low_level_agent" -> low_level_policy (70 -> 17)).  Per transition, on `stream`: the high-level policy acts on
+ * every lane's latest high observation (lanes done at the previous transition: their auto-reset high observation),
+ * the low-level policy on every lane's latest low observation, then one hum_hier_step with HUM_STEP_AUTORESET
+ * steps each lane with the action of the agent it expects (its own level counter, hier_env.py:363-366).  The env
+ * buffers (device, all required) persist across calls: */
+typedef struct {
+    float* obs_high;        /* [n,44] in/out: each lane's latest high-level observation (after hum_hier_reset: its obs) */
+    float* obs_high_reset;  /* [n,44] in/out: the high observation of lanes auto-reset at the last transition */
+    float* obs_low;         /* [n,70] in/out: each lane's latest low-level observation */
+    uint8_t* done;          /* [n] in/out: the last transition's done flags (zeros after hum_hier_reset) */
+    uint8_t* agents;        /* [n] out: agents in the last transition's returned dicts (HUM_AGENT_*) */
+    float* rew_high;        /* [n] out */
+    float* rew_low;         /* [n] out */
+    float* act_high;        /* [n,2] out: the last transition's clipped high-level actions */
+    float* act_low;         /* [n,17] out: the last transition's clipped low-level actions */
+} hum_hier_io;
+/* Per-transition trajectory rows [k,n,...] (device; the struct pointer or any field may be NULL): */
+typedef struct {
+    uint8_t* acted;         /* [k,n] the agent that acted (HUM_AGENT_HIGH / HUM_AGENT_LOW) */
+    float* obs_high;        /* [k,n,44] the high policy's inputs */
+    float* act_high;        /* [k,n,2] its samples before clip_actions (what RLlib's SampleBatch records) */
+    float* obs_low;         /* [k,n,70] the low policy's inputs */
+    float* act_low;         /* [k,n,17] its samples before clip_actions */
+    uint8_t* agents;        /* [k,n] agents in the returned dicts */
+    float* rew_high;        /* [k,n] */
+    float* rew_low;         /* [k,n] */
+    uint8_t* done;          /* [k,n] */
+} hum_hier_traj;
+/* Equal, bitwise, to the loop hum_policy_act_ex(high) ; hum_policy_act_ex(low) ; hum_hier_step(agent = NULL,
+ * HUM_STEP_AUTORESET) driven step by step (noise step index step0 + t for both policies, each with its own seed).
+ * Needs a hierarchical handle, a (44, 2) and a (70, 17) policy on its device (HUM_ERR_ARG / _STATE otherwise).
+ * Replaces: RLlib's multi-agent sampler loop over HierarchicalHumanoidEnv (Train Ray RLLib Hierarchical.py:48-88). */
+int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
+                     const hum_hier_io* io, const hum_hier_traj* traj, void* stream);
 
 /* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
 int hum_get_aux(hum_env* env, float* aux_out, void* stream);

@@ -130,6 +130,7 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         dp = ctypes.POINTER(ctypes.c_double)
         _lib.om_step.argtypes = [ctypes.POINTER(OmParams), dp, dp, ctypes.POINTER(ctypes.c_int)]
+        _lib.om_step_f32.argtypes = [ctypes.POINTER(OmParams), dp, dp, ctypes.POINTER(ctypes.c_int)]
         _lib.om_parts.argtypes = [dp, dp]
         _lib.om_aba.argtypes = [ctypes.POINTER(OmParams), dp, dp, dp]
         _lib.om_mass_matrix.argtypes = [dp, dp]
@@ -150,13 +151,16 @@ def default_params():
     return P
 
 
-def phys_step(state, tau_motor, params=None):
-    """One env step of physics (4 substeps) from a 47-state; returns the new state."""
+def phys_step(state, tau_motor, params=None, precision="fp64"):
+    """One env step of physics (4 substeps) from a 47-state; returns the new state.  precision "fp32": the same
+    restatement instantiated in float arithmetic (physics_oracle_f32.c; state and torques rounded to float on entry),
+    the yardstick for the fp32 kernel's rounding error."""
     P = params or default_params()
     st = np.array(state, dtype=np.float64).copy()
     tau = np.ascontiguousarray(tau_motor, dtype=np.float64)
     nc = ctypes.c_int(0)
-    lib().om_step(ctypes.byref(P), _p(st), _p(tau), ctypes.byref(nc))
+    fn = lib().om_step_f32 if precision == "fp32" else lib().om_step
+    fn(ctypes.byref(P), _p(st), _p(tau), ctypes.byref(nc))
     return st
 
 
@@ -318,9 +322,11 @@ def get_joint_pos(clip, row, joint):
 class OracleLowLevelEnv:
     """Single-lane restatement of LowLevelHumanoidEnv (low_level_env.py:36-526)."""
 
-    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=DEFAULT_NUMPY, terrain=None):
+    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=DEFAULT_NUMPY, terrain=None,
+                 phys_precision="fp64"):
         self.clip = clip
         self.params = params
+        self.phys_precision = phys_precision   # "fp32": physics through the float instantiation (phys_step)
         self.terrain = terrain          # None / Terrain (LowLevelHumanoidEnv(useCustomEnv=True): CustomScene)
         self.terrain_key = 0
         self.numpy_semantics = numpy_semantics
@@ -373,11 +379,11 @@ class OracleLowLevelEnv:
         self.delta_highTargetScore = 0
 
     @classmethod
-    def from_lane(cls, clip, phys, book, bk, numpy_semantics=DEFAULT_NUMPY):
+    def from_lane(cls, clip, phys, book, bk, numpy_semantics=DEFAULT_NUMPY, phys_precision="fp64"):
         """An env holding exactly one product lane's state: phys [47] and book [HUM_NBOOK] as hum_get_state
         returns them, bk = the HUM_BK_* column map (ilrl_amd._native.BK, passed in: the oracle imports nothing
         from the product).  Its RNG continues the lane's stream (key words + counter)."""
-        o = cls(clip, numpy_semantics=numpy_semantics)
+        o = cls(clip, numpy_semantics=numpy_semantics, phys_precision=phys_precision)
         o.state = np.array(phys, dtype=np.float64).copy()
         o.frame = int(book[bk["frame"]])
         o.cur_timestep = int(book[bk["cur_timestep"]])
@@ -597,7 +603,8 @@ class OracleLowLevelEnv:
     def step(self, action, debug=False, physics=True):              # :475-526
         action = np.asarray(action, dtype=np.float32)
         if physics:
-            self.state = phys_step(self.state, motor_torques(action, self.numpy_semantics), self._phys_params())
+            self.state = phys_step(self.state, motor_torques(action, self.numpy_semantics), self._phys_params(),
+                                   self.phys_precision)
         self.cur_obs = self._calc_state()
         self.robot_pos[0] = self.body_xyz[0]
         self.robot_pos[1] = self.body_xyz[1]

@@ -27,9 +27,11 @@ class OracleHierEnv:
     """Single-lane restatement of HierarchicalHumanoidEnv (hier_env.py:38-641).  `clip` is the selected motion
     (motion_list[selected_motion] = motion09_03, hier_env.py:50,179)."""
 
-    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=O.DEFAULT_NUMPY):
+    def __init__(self, clip, seed=0, lane=0, params=None, rng=None, numpy_semantics=O.DEFAULT_NUMPY,
+                 phys_precision="fp64"):
         self.clip = clip
         self.params = params
+        self.phys_precision = phys_precision   # "fp32": physics through the float instantiation (O.phys_step)
         self.numpy_semantics = numpy_semantics
         self.step_per_level = 5                                     # :58
         self.steps_remaining_at_level = self.step_per_level
@@ -59,12 +61,12 @@ class OracleHierEnv:
         self.initReward()
 
     @classmethod
-    def from_lane(cls, clip, phys, book, bk, numpy_semantics=O.DEFAULT_NUMPY):
+    def from_lane(cls, clip, phys, book, bk, numpy_semantics=O.DEFAULT_NUMPY, phys_precision="fp64"):
         """An env holding exactly one product lane's state (hum_get_state rows; bk = the HUM_BK_* column map, passed
         in: the oracle imports nothing from the product).  cur_obs is the calc_state of that state under the lane's
         walk target, which is what the reference holds between calls (its walk target changes only in
         high_level_step and resetFromFrame, after which cur_obs is not recomputed until the next low step)."""
-        o = cls(clip, numpy_semantics=numpy_semantics)
+        o = cls(clip, numpy_semantics=numpy_semantics, phys_precision=phys_precision)
         o.state = np.array(phys, dtype=np.float64).copy()
         o.selected_motion_frame = int(book[bk["frame"]])
         o.cur_timestep = int(book[bk["cur_timestep"]])
@@ -322,7 +324,8 @@ class OracleHierEnv:
         action = np.asarray(action, dtype=np.float32)
         self.steps_remaining_at_level -= 1
         if physics:
-            self.state = O.phys_step(self.state, O.motor_torques(action, self.numpy_semantics), self.params)
+            self.state = O.phys_step(self.state, O.motor_torques(action, self.numpy_semantics), self.params,
+                                     self.phys_precision)
         self.cur_obs = self._calc_state()
         self.updateReward(action=action)
         reward = [self.deltaJoints, self.deltaVelJoints, self.delta_lowTargetScore, self.electricityScore,

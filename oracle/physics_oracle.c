@@ -32,11 +32,65 @@
  * State vector (47 doubles, shared with the product C-ABI): base pos[3] (COM, world), base quat[4]
  * (x,y,z,w), base lin vel[3] (COM, world), base ang vel[3] (world), q[17], qd[17] (XML dof order).
  */
-#include <math.h>
 #include <string.h>
+#include <tgmath.h>   /* sqrt / sin / cos / floor / fabs follow `real` */
 
 #include "humanoid_links_gen.h"
 #include "physics_oracle.h"
+
+/* `real` is the arithmetic type of the whole restatement: double here; physics_oracle_f32.c re-includes this
+ * file with OM_F32 (real = float, every literal single precision via -fsingle-precision-constant, the model
+ * constants rounded to float once) - the same algorithm in float arithmetic, the yardstick for the fp32 kernel's
+ * rounding error (tests/test_gpu_scale.py). */
+#ifdef OM_F32
+typedef float real;
+#define OM_F32_TABLES(X) X(om_Rfix, 288) X(om_t, 96) X(om_axis, 96) X(om_mass, 32) X(om_com, 96) X(om_inertia, 288) \
+    X(om_lo, 17) X(om_hi, 17) X(om_jdamp, 17) X(om_gr, 17) X(om_gp1, 51) X(om_gp2, 51) X(om_part_p, 99)
+#define OM_F32_DECL(name, n) static float name##_f[n];
+OM_F32_TABLES(OM_F32_DECL)
+__attribute__((constructor)) static void om_f32_tables(void) {
+#define OM_F32_COPY(name, n) for (int i = 0; i < n; i++) name##_f[i] = (float)name[i];
+    OM_F32_TABLES(OM_F32_COPY)
+}
+#define om_Rfix om_Rfix_f
+#define om_t om_t_f
+#define om_axis om_axis_f
+#define om_mass om_mass_f
+#define om_com om_com_f
+#define om_inertia om_inertia_f
+#define om_lo om_lo_f
+#define om_hi om_hi_f
+#define om_jdamp om_jdamp_f
+#define om_gr om_gr_f
+#define om_gp1 om_gp1_f
+#define om_gp2 om_gp2_f
+#define om_part_p om_part_p_f
+float om_block_height(unsigned long long key, int bi, int bj);   /* the terrain draw stays the double TU's */
+#define block_height om_block_height
+#else
+typedef double real;
+#endif
+
+/* om_params in the arithmetic type */
+typedef struct {
+    real dt, gravity, erp_contact, erp_limit, mu_ground, mu_self, contact_thresh, lin_damp, ang_damp;
+    real limit_max_impulse, max_coord_vel, hf_s[3], hf_o[3], hf_mid, split_pen;
+    int nsub, iters, max_contacts, self_collision, joint_damping, terrain, hf_w, hf_l;
+    const float* hf;
+    unsigned long long terrain_key;
+} rparams;
+
+static void to_rparams(const om_params* P, rparams* Q) {
+    Q->dt = (real)P->dt; Q->gravity = (real)P->gravity; Q->erp_contact = (real)P->erp_contact;
+    Q->erp_limit = (real)P->erp_limit; Q->mu_ground = (real)P->mu_ground; Q->mu_self = (real)P->mu_self;
+    Q->contact_thresh = (real)P->contact_thresh; Q->lin_damp = (real)P->lin_damp; Q->ang_damp = (real)P->ang_damp;
+    Q->limit_max_impulse = (real)P->limit_max_impulse; Q->max_coord_vel = (real)P->max_coord_vel;
+    for (int k = 0; k < 3; k++) { Q->hf_s[k] = (real)P->hf_s[k]; Q->hf_o[k] = (real)P->hf_o[k]; }
+    Q->hf_mid = (real)P->hf_mid; Q->split_pen = (real)P->split_pen;
+    Q->nsub = P->nsub; Q->iters = P->iters; Q->max_contacts = P->max_contacts; Q->self_collision = P->self_collision;
+    Q->joint_damping = P->joint_damping; Q->terrain = P->terrain; Q->hf_w = P->hf_w; Q->hf_l = P->hf_l;
+    Q->hf = P->hf; Q->terrain_key = P->terrain_key;
+}
 
 #define NV (6 + OM_ND)
 /* contact list capacity: every candidate fits (29 sphere / capsule-end ground points + 66 geom pairs = 95), so
@@ -46,38 +100,38 @@
 
 
 /* ------------------------------------------------------------------------- small linear algebra */
-static void mat3_mul(const double* A, const double* B, double* C) {
-    double T[9];
+static void mat3_mul(const real* A, const real* B, real* C) {
+    real T[9];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
     memcpy(C, T, sizeof T);
 }
-static void mat3_vec(const double* A, const double* x, double* y) {
-    double t[3];
+static void mat3_vec(const real* A, const real* x, real* y) {
+    real t[3];
     for (int i = 0; i < 3; i++) t[i] = A[3 * i] * x[0] + A[3 * i + 1] * x[1] + A[3 * i + 2] * x[2];
     memcpy(y, t, sizeof t);
 }
-static void mat3T_vec(const double* A, const double* x, double* y) {
-    double t[3];
+static void mat3T_vec(const real* A, const real* x, real* y) {
+    real t[3];
     for (int i = 0; i < 3; i++) t[i] = A[i] * x[0] + A[3 + i] * x[1] + A[6 + i] * x[2];
     memcpy(y, t, sizeof t);
 }
-static void cross(const double* a, const double* b, double* c) {
-    double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+static void cross(const real* a, const real* b, real* c) {
+    real t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
     memcpy(c, t, sizeof t);
 }
-static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-static double norm3(const double* a) { return sqrt(dot3(a, a)); }
+static real dot3(const real* a, const real* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static real norm3(const real* a) { return sqrt(dot3(a, a)); }
 
-static void axis_angle(const double* u, double q, double* R) {
-    double c = cos(q), s = sin(q), C = 1 - c;
-    double x = u[0], y = u[1], z = u[2];
+static void axis_angle(const real* u, real q, real* R) {
+    real c = cos(q), s = sin(q), C = 1 - c;
+    real x = u[0], y = u[1], z = u[2];
     R[0] = c + x * x * C;     R[1] = x * y * C - z * s; R[2] = x * z * C + y * s;
     R[3] = y * x * C + z * s; R[4] = c + y * y * C;     R[5] = y * z * C - x * s;
     R[6] = z * x * C - y * s; R[7] = z * y * C + x * s; R[8] = c + z * z * C;
 }
-static void quat_to_mat(const double* q, double* R) { /* q = x,y,z,w */
-    double x = q[0], y = q[1], z = q[2], w = q[3];
+static void quat_to_mat(const real* q, real* R) { /* q = x,y,z,w */
+    real x = q[0], y = q[1], z = q[2], w = q[3];
     R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z);     R[2] = 2 * (x * z + w * y);
     R[3] = 2 * (x * y + w * z);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
     R[6] = 2 * (x * z - w * y);     R[7] = 2 * (y * z + w * x);     R[8] = 1 - 2 * (x * x + y * y);
@@ -85,19 +139,19 @@ static void quat_to_mat(const double* q, double* R) { /* q = x,y,z,w */
 
 /* --------------------------------------------------------------------------- kinematics */
 typedef struct {
-    double R[OM_NL][9];   /* link frame -> world */
-    double x[OM_NL][3];   /* link origin, world */
-    double E[OM_NL][9];   /* parent coords -> link coords (rotation part of X) */
+    real R[OM_NL][9];   /* link frame -> world */
+    real x[OM_NL][3];   /* link origin, world */
+    real E[OM_NL][9];   /* parent coords -> link coords (rotation part of X) */
 } om_kin;
 
-static void fk(const double* st, om_kin* K) {
+static void fk(const real* st, om_kin* K) {
     quat_to_mat(st + 3, K->R[0]);
-    memcpy(K->x[0], st, 3 * sizeof(double));
+    memcpy(K->x[0], st, 3 * sizeof(real));
     for (int l = 1; l < OM_NL; l++) {
         int p = om_parent[l];
-        double Rl[9];
+        real Rl[9];
         if (om_type[l] == 1) {
-            double Ra[9];
+            real Ra[9];
             axis_angle(om_axis + 3 * l, st[13 + om_dof[l]], Ra);
             mat3_mul(om_Rfix + 9 * l, Ra, Rl);       /* parent <- link */
         } else {
@@ -106,27 +160,29 @@ static void fk(const double* st, om_kin* K) {
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) K->E[l][3 * i + j] = Rl[3 * j + i];   /* transpose: link <- parent */
         mat3_mul(K->R[p], Rl, K->R[l]);
-        double d[3];
+        real d[3];
         mat3_vec(K->R[p], om_t + 3 * l, d);
         for (int i = 0; i < 3; i++) K->x[l][i] = K->x[p][i] + d[i];
     }
 }
 
+#ifndef OM_F32
 void om_parts(const double* st, double* out /* [OM_NPART][3] */) {
     om_kin K;
     fk(st, &K);
     for (int k = 0; k < OM_NPART; k++) {
         int l = om_part_link[k];
         if (l < 0) { out[3 * k] = out[3 * k + 1] = out[3 * k + 2] = 0.0; continue; }
-        double d[3];
+        real d[3];
         mat3_vec(K.R[l], om_part_p + 3 * k, d);
         for (int i = 0; i < 3; i++) out[3 * k + i] = K.x[l][i] + d[i];
     }
 }
+#endif
 
 /* world position of a point given in link coords */
-static void link_point(const om_kin* K, int l, const double* p, double* w) {
-    double d[3];
+static void link_point(const om_kin* K, int l, const real* p, real* w) {
+    real d[3];
     mat3_vec(K->R[l], p, d);
     for (int i = 0; i < 3; i++) w[i] = K->x[l][i] + d[i];
 }
@@ -134,9 +190,9 @@ static void link_point(const om_kin* K, int l, const double* p, double* w) {
 /* --------------------------------------------------------------------------- Jacobians / mass matrix */
 /* Generalised velocity nu = [w(3) world, v(3) base COM world, qd(ND)]. */
 /* point Jacobian (3 x NV, row major) of a world point p rigidly attached to link l */
-static void point_jacobian(const om_kin* K, int l, const double* p, double* J) {
-    memset(J, 0, 3 * NV * sizeof(double));
-    double d[3] = {p[0] - K->x[0][0], p[1] - K->x[0][1], p[2] - K->x[0][2]};
+static void point_jacobian(const om_kin* K, int l, const real* p, real* J) {
+    memset(J, 0, 3 * NV * sizeof(real));
+    real d[3] = {p[0] - K->x[0][0], p[1] - K->x[0][1], p[2] - K->x[0][2]};
     /* w x d = -d x w  -> columns of -[d]x */
     J[0 * NV + 0] = 0;     J[0 * NV + 1] = d[2];  J[0 * NV + 2] = -d[1];
     J[1 * NV + 0] = -d[2]; J[1 * NV + 1] = 0;     J[1 * NV + 2] = d[0];
@@ -144,7 +200,7 @@ static void point_jacobian(const om_kin* K, int l, const double* p, double* J) {
     J[0 * NV + 3] = 1; J[1 * NV + 4] = 1; J[2 * NV + 5] = 1;
     for (int k = l; k > 0; k = om_parent[k]) {
         if (om_type[k] != 1) continue;
-        double u[3], r[3], c[3];
+        real u[3], r[3], c[3];
         mat3_vec(K->R[k], om_axis + 3 * k, u);
         for (int i = 0; i < 3; i++) r[i] = p[i] - K->x[k][i];
         cross(u, r, c);
@@ -152,25 +208,25 @@ static void point_jacobian(const om_kin* K, int l, const double* p, double* J) {
         for (int i = 0; i < 3; i++) J[i * NV + col] = c[i];
     }
 }
-static void ang_jacobian(const om_kin* K, int l, double* J) {
-    memset(J, 0, 3 * NV * sizeof(double));
+static void ang_jacobian(const om_kin* K, int l, real* J) {
+    memset(J, 0, 3 * NV * sizeof(real));
     J[0 * NV + 0] = 1; J[1 * NV + 1] = 1; J[2 * NV + 2] = 1;
     for (int k = l; k > 0; k = om_parent[k]) {
         if (om_type[k] != 1) continue;
-        double u[3];
+        real u[3];
         mat3_vec(K->R[k], om_axis + 3 * k, u);
         int col = 6 + om_dof[k];
         for (int i = 0; i < 3; i++) J[i * NV + col] = u[i];
     }
 }
 
-static void mass_matrix(const om_kin* K, double* H) {
-    memset(H, 0, NV * NV * sizeof(double));
-    double Jp[3 * NV], Jw[3 * NV];
+static void mass_matrix(const om_kin* K, real* H) {
+    memset(H, 0, NV * NV * sizeof(real));
+    real Jp[3 * NV], Jw[3 * NV];
     for (int l = 0; l < OM_NL; l++) {
-        double m = om_mass[l];
+        real m = om_mass[l];
         if (m <= 0) continue;
-        double c[3], Iw[9], T[9], RT[9];
+        real c[3], Iw[9], T[9], RT[9];
         link_point(K, l, om_com + 3 * l, c);
         point_jacobian(K, l, c, Jp);
         ang_jacobian(K, l, Jw);
@@ -180,7 +236,7 @@ static void mass_matrix(const om_kin* K, double* H) {
         mat3_mul(T, RT, Iw);
         for (int a = 0; a < NV; a++)
             for (int b = 0; b < NV; b++) {
-                double s = 0;
+                real s = 0;
                 for (int i = 0; i < 3; i++) s += m * Jp[i * NV + a] * Jp[i * NV + b];
                 for (int i = 0; i < 3; i++)
                     for (int j = 0; j < 3; j++) s += Jw[i * NV + a] * Iw[3 * i + j] * Jw[j * NV + b];
@@ -189,28 +245,28 @@ static void mass_matrix(const om_kin* K, double* H) {
     }
 }
 
-static int cholesky(double* A, int n) { /* in place, lower */
+static int cholesky(real* A, int n) { /* in place, lower */
     for (int j = 0; j < n; j++) {
-        double s = A[j * n + j];
+        real s = A[j * n + j];
         for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
         if (s <= 0) return -1;
         A[j * n + j] = sqrt(s);
         for (int i = j + 1; i < n; i++) {
-            double t = A[i * n + j];
+            real t = A[i * n + j];
             for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
             A[i * n + j] = t / A[j * n + j];
         }
     }
     return 0;
 }
-static void chol_solve(const double* L, int n, double* b) {
+static void chol_solve(const real* L, int n, real* b) {
     for (int i = 0; i < n; i++) {
-        double s = b[i];
+        real s = b[i];
         for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
         b[i] = s / L[i * n + i];
     }
     for (int i = n - 1; i >= 0; i--) {
-        double s = b[i];
+        real s = b[i];
         for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
         b[i] = s / L[i * n + i];
     }
@@ -218,16 +274,16 @@ static void chol_solve(const double* L, int n, double* b) {
 
 /* --------------------------------------------------------------------------- spatial algebra (local frames) */
 /* motion/force 6-vectors are [angular; linear]. */
-static void crm(const double* v, const double* m, double* r) { /* v x m */
-    double a[3], b[3], c[3];
+static void crm(const real* v, const real* m, real* r) { /* v x m */
+    real a[3], b[3], c[3];
     cross(v, m, a);
     cross(v, m + 3, b);
     cross(v + 3, m, c);
     r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
     r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
 }
-static void crf(const double* v, const double* f, double* r) { /* v x* f */
-    double a[3], b[3], c[3];
+static void crf(const real* v, const real* f, real* r) { /* v x* f */
+    real a[3], b[3], c[3];
     cross(v, f, a);
     cross(v + 3, f + 3, b);
     cross(v, f + 3, c);
@@ -235,13 +291,13 @@ static void crf(const double* v, const double* f, double* r) { /* v x* f */
     r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
 }
 /* spatial inertia at link origin, link coords, 6x6 row major */
-static void spatial_inertia(int l, double* I6) {
-    double m = om_mass[l];
-    const double* c = om_com + 3 * l;
-    const double* Ic = om_inertia + 9 * l;
-    double cc = dot3(c, c);
-    double cx[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
-    memset(I6, 0, 36 * sizeof(double));
+static void spatial_inertia(int l, real* I6) {
+    real m = om_mass[l];
+    const real* c = om_com + 3 * l;
+    const real* Ic = om_inertia + 9 * l;
+    real cc = dot3(c, c);
+    real cx[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+    memset(I6, 0, 36 * sizeof(real));
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) {
             I6[6 * i + j] = Ic[3 * i + j] + m * ((i == j ? cc : 0) - c[i] * c[j]);
@@ -250,21 +306,21 @@ static void spatial_inertia(int l, double* I6) {
             I6[6 * (3 + i) + 3 + j] = (i == j) ? m : 0;
         }
 }
-static void mat6_vec(const double* A, const double* x, double* y) {
-    double t[6];
+static void mat6_vec(const real* A, const real* x, real* y) {
+    real t[6];
     for (int i = 0; i < 6; i++) {
-        double s = 0;
+        real s = 0;
         for (int j = 0; j < 6; j++) s += A[6 * i + j] * x[j];
         t[i] = s;
     }
     memcpy(y, t, sizeof t);
 }
 /* X (parent->link) as a full 6x6: [[E,0],[-E rx, E]] */
-static void build_X(const double* E, const double* r, double* X) {
-    double rx[9] = {0, -r[2], r[1], r[2], 0, -r[0], -r[1], r[0], 0};
-    double Erx[9];
+static void build_X(const real* E, const real* r, real* X) {
+    real rx[9] = {0, -r[2], r[1], r[2], 0, -r[0], -r[1], r[0], 0};
+    real Erx[9];
     mat3_mul(E, rx, Erx);
-    memset(X, 0, 36 * sizeof(double));
+    memset(X, 0, 36 * sizeof(real));
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) {
             X[6 * i + j] = E[3 * i + j];
@@ -275,12 +331,12 @@ static void build_X(const double* E, const double* r, double* X) {
 
 /* ABA: generalised accelerations (nu-dot, base classical accel in world) for state st, joint torques tau.
  * Returns acc[NV] = [w_dot world, v_com_dot world, qdd]. */
-static void aba(const om_params* P, const double* st, const om_kin* K, const double* tau, double* acc) {
-    double X[OM_NL][36], v[OM_NL][6], c[OM_NL][6], IA[OM_NL][36], pA[OM_NL][6];
-    double U[OM_NL][6], D[OM_NL], u[OM_NL], a[OM_NL][6];
-    const double g[3] = {0, 0, -P->gravity};
+static void aba(const rparams* P, const real* st, const om_kin* K, const real* tau, real* acc) {
+    real X[OM_NL][36], v[OM_NL][6], c[OM_NL][6], IA[OM_NL][36], pA[OM_NL][6];
+    real U[OM_NL][6], D[OM_NL], u[OM_NL], a[OM_NL][6];
+    const real g[3] = {0, 0, -P->gravity};
     /* base velocity in base coords */
-    double wl[3], vl[3];
+    real wl[3], vl[3];
     mat3T_vec(K->R[0], st + 10, wl);
     mat3T_vec(K->R[0], st + 7, vl);
     for (int l = 0; l < OM_NL; l++) {
@@ -294,32 +350,32 @@ static void aba(const om_params* P, const double* st, const om_kin* K, const dou
             mat6_vec(X[l], v[p], v[l]);
             memset(c[l], 0, sizeof c[l]);
             if (om_type[l] == 1) {
-                double qd = st[30 + om_dof[l]];
-                double Sq[6] = {om_axis[3 * l] * qd, om_axis[3 * l + 1] * qd, om_axis[3 * l + 2] * qd, 0, 0, 0};
+                real qd = st[30 + om_dof[l]];
+                real Sq[6] = {om_axis[3 * l] * qd, om_axis[3 * l + 1] * qd, om_axis[3 * l + 2] * qd, 0, 0, 0};
                 for (int i = 0; i < 6; i++) v[l][i] += Sq[i];
                 crm(v[l], Sq, c[l]);
             }
         }
         spatial_inertia(l, IA[l]);
-        double Iv[6];
+        real Iv[6];
         mat6_vec(IA[l], v[l], Iv);
         crf(v[l], Iv, pA[l]);
         /* external: gravity + Bullet link damping, applied at the COM */
-        double m = om_mass[l];
+        real m = om_mass[l];
         if (m > 0) {
-            const double* cm = om_com + 3 * l;
-            double gl[3], vcom[3], wxc[3], F[3], n[3], Iw[3];
+            const real* cm = om_com + 3 * l;
+            real gl[3], vcom[3], wxc[3], F[3], n[3], Iw[3];
             mat3T_vec(K->R[l], g, gl);
             cross(v[l], cm, wxc);
             for (int i = 0; i < 3; i++) vcom[i] = v[l][3 + i] + wxc[i];
-            double kv = P->lin_damp + P->lin_damp * norm3(vcom);
-            double kw = P->ang_damp + P->ang_damp * norm3(v[l]);
+            real kv = P->lin_damp + P->lin_damp * norm3(vcom);
+            real kw = P->ang_damp + P->ang_damp * norm3(v[l]);
             mat3_vec(om_inertia + 9 * l, v[l], Iw);
             for (int i = 0; i < 3; i++) {
                 F[i] = m * gl[i] - m * vcom[i] * kv;
                 n[i] = -Iw[i] * kw;
             }
-            double cxF[3];
+            real cxF[3];
             cross(cm, F, cxF);
             for (int i = 0; i < 3; i++) {
                 pA[l][i] -= n[i] + cxF[i];
@@ -329,56 +385,56 @@ static void aba(const om_params* P, const double* st, const om_kin* K, const dou
     }
     for (int l = OM_NL - 1; l >= 1; l--) {
         int p = om_parent[l];
-        double Ia[36], pa[6];
+        real Ia[36], pa[6];
         memcpy(Ia, IA[l], sizeof Ia);
         memcpy(pa, pA[l], sizeof pa);
         if (om_type[l] == 1) {
-            const double* ax = om_axis + 3 * l;
-            double S[6] = {ax[0], ax[1], ax[2], 0, 0, 0};
+            const real* ax = om_axis + 3 * l;
+            real S[6] = {ax[0], ax[1], ax[2], 0, 0, 0};
             mat6_vec(IA[l], S, U[l]);
             D[l] = 0;
             for (int i = 0; i < 6; i++) D[l] += S[i] * U[l][i];
-            double Sp = 0;
+            real Sp = 0;
             for (int i = 0; i < 6; i++) Sp += S[i] * pA[l][i];
             u[l] = tau[om_dof[l]] - Sp;
             if (P->joint_damping) {   /* implicit Euler on -d*qd: (D + dt d) qdd = u - d qd */
-                double dmp = om_jdamp[om_dof[l]];
+                real dmp = om_jdamp[om_dof[l]];
                 D[l] += P->dt * dmp;
                 u[l] -= dmp * st[30 + om_dof[l]];
             }
             for (int i = 0; i < 6; i++)
                 for (int j = 0; j < 6; j++) Ia[6 * i + j] -= U[l][i] * U[l][j] / D[l];
-            double Iac[6];
+            real Iac[6];
             mat6_vec(Ia, c[l], Iac);
             for (int i = 0; i < 6; i++) pa[i] = pA[l][i] + Iac[i] + U[l][i] * u[l] / D[l];
         } else {
-            double Iac[6];
+            real Iac[6];
             mat6_vec(Ia, c[l], Iac);
             for (int i = 0; i < 6; i++) pa[i] += Iac[i];
         }
         /* IA_p += X^T Ia X ; pA_p += X^T pa */
-        double T[36];
+        real T[36];
         for (int i = 0; i < 6; i++)
             for (int j = 0; j < 6; j++) {
-                double s = 0;
+                real s = 0;
                 for (int k = 0; k < 6; k++) s += Ia[6 * i + k] * X[l][6 * k + j];
                 T[6 * i + j] = s;
             }
         for (int i = 0; i < 6; i++)
             for (int j = 0; j < 6; j++) {
-                double s = 0;
+                real s = 0;
                 for (int k = 0; k < 6; k++) s += X[l][6 * k + i] * T[6 * k + j];
                 IA[p][6 * i + j] += s;
             }
         for (int i = 0; i < 6; i++) {
-            double s = 0;
+            real s = 0;
             for (int k = 0; k < 6; k++) s += X[l][6 * k + i] * pa[k];
             pA[p][i] += s;
         }
     }
     /* base: a0 = -IA0^{-1} pA0 */
     {
-        double L[36], b[6];
+        real L[36], b[6];
         memcpy(L, IA[0], sizeof L);
         cholesky(L, 6);
         for (int i = 0; i < 6; i++) b[i] = -pA[0][i];
@@ -387,24 +443,24 @@ static void aba(const om_params* P, const double* st, const om_kin* K, const dou
     }
     for (int l = 1; l < OM_NL; l++) {
         int p = om_parent[l];
-        double ap[6];
+        real ap[6];
         mat6_vec(X[l], a[p], ap);
         for (int i = 0; i < 6; i++) a[l][i] = ap[i] + c[l][i];
         if (om_type[l] == 1) {
-            double Ua = 0;
+            real Ua = 0;
             for (int i = 0; i < 6; i++) Ua += U[l][i] * a[l][i];
-            double qdd = (u[l] - Ua) / D[l];
+            real qdd = (u[l] - Ua) / D[l];
             acc[6 + om_dof[l]] = qdd;
-            const double* ax = om_axis + 3 * l;
+            const real* ax = om_axis + 3 * l;
             a[l][0] += ax[0] * qdd; a[l][1] += ax[1] * qdd; a[l][2] += ax[2] * qdd;
         }
     }
     /* base: spatial -> classical, base coords -> world */
-    double wd[3], lin[3], wxv[3];
+    real wd[3], lin[3], wxv[3];
     cross(wl, vl, wxv);
     for (int i = 0; i < 3; i++) lin[i] = a[0][3 + i] + wxv[i];
     mat3_vec(K->R[0], a[0], wd);
-    double ld[3];
+    real ld[3];
     mat3_vec(K->R[0], lin, ld);
     for (int i = 0; i < 3; i++) { acc[i] = wd[i]; acc[3 + i] = ld[i]; }
 }
@@ -412,28 +468,28 @@ static void aba(const om_params* P, const double* st, const om_kin* K, const dou
 /* --------------------------------------------------------------------------- collision */
 typedef struct {
     int la, lb;         /* links; lb = -1 for ground */
-    double pa[3], pb[3]; /* contact points on A and B (world) */
-    double n[3];        /* normal, from B to A */
-    double d;           /* signed distance (<0 penetration) */
-    double mu;
+    real pa[3], pb[3]; /* contact points on A and B (world) */
+    real n[3];        /* normal, from B to A */
+    real d;           /* signed distance (<0 penetration) */
+    real mu;
 } om_contact;
 
-static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static real clampd(real x, real lo, real hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 /* closest points between segments p1q1 and p2q2 (Ericson, Real-Time Collision Detection 5.1.9) */
-static void seg_seg(const double* p1, const double* q1, const double* p2, const double* q2, double* c1, double* c2) {
-    double d1[3], d2[3], r[3];
+static void seg_seg(const real* p1, const real* q1, const real* p2, const real* q2, real* c1, real* c2) {
+    real d1[3], d2[3], r[3];
     for (int i = 0; i < 3; i++) { d1[i] = q1[i] - p1[i]; d2[i] = q2[i] - p2[i]; r[i] = p1[i] - p2[i]; }
-    double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
-    double s, t;
-    const double EPS = 1e-12;
+    real a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    real s, t;
+    const real EPS = 1e-12;
     if (a <= EPS && e <= EPS) { s = t = 0; }
     else if (a <= EPS) { s = 0; t = clampd(f / e, 0, 1); }
     else {
-        double c = dot3(d1, r);
+        real c = dot3(d1, r);
         if (e <= EPS) { t = 0; s = clampd(-c / a, 0, 1); }
         else {
-            double b = dot3(d1, d2), den = a * e - b * b;
+            real b = dot3(d1, d2), den = a * e - b * b;
             s = (den > EPS) ? clampd((b * f - c * e) / den, 0, 1) : 0;
             t = (b * s + f) / e;
             if (t < 0) { t = 0; s = clampd(-c / a, 0, 1); }
@@ -449,22 +505,28 @@ static void seg_seg(const double* p1, const double* q1, const double* p2, const 
  * even, along (i+1,j)-(i,j+1) otherwise.  A ground candidate sphere touches the closest point of the surface
  * over the triangles of the cells within reach; a centre below the plane of the triangle under it takes that
  * triangle's upward normal. */
+#ifndef OM_F32
 static unsigned long long sm64(unsigned long long z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-static float block_height(unsigned long long key, int bi, int bj) {   /* humanoid.py:94-111 */
+#endif
+#ifndef OM_F32
+float om_block_height(unsigned long long key, int bi, int bj);
+float om_block_height(unsigned long long key, int bi, int bj) {   /* humanoid.py:94-111 */
     if ((bi == 63 || bi == 64) && (bj == 63 || bj == 64)) return 0.f;
     double u = (double)(sm64(key + (unsigned long long)(bi + 128 * bj)) >> 11) * (1.0 / 9007199254740992.0);
     return (float)((0.05 * u) * 10.0);
 }
-static void hf_vertex(const om_params* P, int i, int j, double* v) {
+#define block_height om_block_height
+#endif
+static void hf_vertex(const rparams* P, int i, int j, real* v) {
     float h = P->terrain == 1 ? P->hf[i + j * P->hf_w] : block_height(P->terrain_key, i >> 1, j >> 1);
-    v[0] = ((double)i - 0.5 * (P->hf_w - 1)) * P->hf_s[0] + P->hf_o[0];
-    v[1] = ((double)j - 0.5 * (P->hf_l - 1)) * P->hf_s[1] + P->hf_o[1];
-    v[2] = ((double)h - P->hf_mid) * P->hf_s[2] + P->hf_o[2];
+    v[0] = ((real)i - 0.5 * (P->hf_w - 1)) * P->hf_s[0] + P->hf_o[0];
+    v[1] = ((real)j - 0.5 * (P->hf_l - 1)) * P->hf_s[1] + P->hf_o[1];
+    v[2] = ((real)h - P->hf_mid) * P->hf_s[2] + P->hf_o[2];
 }
 static void tri_corners(int ci, int cj, int t, int* di, int* dj) {
     static const int A[2][2][6] = {{{0, 0, 1, 0, 1, 1}, {0, 1, 1, 0, 1, 0}}, {{0, 0, 1, 0, 1, 0}, {1, 0, 1, 0, 1, 1}}};
@@ -472,35 +534,35 @@ static void tri_corners(int ci, int cj, int t, int* di, int* dj) {
     for (int k = 0; k < 3; k++) { di[k] = o[k]; dj[k] = o[3 + k]; }
 }
 /* closest point of triangle abc to p (Ericson 5.1.5) */
-static void closest_tri(const double* p, const double* a, const double* b, const double* c, double* q) {
-    double ab[3], ac[3], ap[3], bp[3], cp[3];
+static void closest_tri(const real* p, const real* a, const real* b, const real* c, real* q) {
+    real ab[3], ac[3], ap[3], bp[3], cp[3];
     for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ap[k] = p[k] - a[k]; }
-    double d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-    if (d1 <= 0 && d2 <= 0) { memcpy(q, a, 3 * sizeof(double)); return; }
+    real d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+    if (d1 <= 0 && d2 <= 0) { memcpy(q, a, 3 * sizeof(real)); return; }
     for (int k = 0; k < 3; k++) bp[k] = p[k] - b[k];
-    double d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-    if (d3 >= 0 && d4 <= d3) { memcpy(q, b, 3 * sizeof(double)); return; }
-    double vc = d1 * d4 - d3 * d2;
-    if (vc <= 0 && d1 >= 0 && d3 <= 0) { double t = d1 / (d1 - d3); for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k]; return; }
+    real d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+    if (d3 >= 0 && d4 <= d3) { memcpy(q, b, 3 * sizeof(real)); return; }
+    real vc = d1 * d4 - d3 * d2;
+    if (vc <= 0 && d1 >= 0 && d3 <= 0) { real t = d1 / (d1 - d3); for (int k = 0; k < 3; k++) q[k] = a[k] + t * ab[k]; return; }
     for (int k = 0; k < 3; k++) cp[k] = p[k] - c[k];
-    double d5 = dot3(ab, cp), d6 = dot3(ac, cp);
-    if (d6 >= 0 && d5 <= d6) { memcpy(q, c, 3 * sizeof(double)); return; }
-    double vb = d5 * d2 - d1 * d6;
-    if (vb <= 0 && d2 >= 0 && d6 <= 0) { double t = d2 / (d2 - d6); for (int k = 0; k < 3; k++) q[k] = a[k] + t * ac[k]; return; }
-    double va = d3 * d6 - d5 * d4;
+    real d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+    if (d6 >= 0 && d5 <= d6) { memcpy(q, c, 3 * sizeof(real)); return; }
+    real vb = d5 * d2 - d1 * d6;
+    if (vb <= 0 && d2 >= 0 && d6 <= 0) { real t = d2 / (d2 - d6); for (int k = 0; k < 3; k++) q[k] = a[k] + t * ac[k]; return; }
+    real va = d3 * d6 - d5 * d4;
     if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-        double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        real t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
         for (int k = 0; k < 3; k++) q[k] = b[k] + t * (c[k] - b[k]);
         return;
     }
-    double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
+    real den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;
     for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
 }
-static int terrain_contact(const om_params* P, const double* c, double r, double* n, double* d) {
-    double u = (c[0] - P->hf_o[0]) / P->hf_s[0] + 0.5 * (P->hf_w - 1);
-    double v = (c[1] - P->hf_o[1]) / P->hf_s[1] + 0.5 * (P->hf_l - 1);
+static int terrain_contact(const rparams* P, const real* c, real r, real* n, real* d) {
+    real u = (c[0] - P->hf_o[0]) / P->hf_s[0] + 0.5 * (P->hf_w - 1);
+    real v = (c[1] - P->hf_o[1]) / P->hf_s[1] + 0.5 * (P->hf_l - 1);
     if (!(u > -2 && u < P->hf_w + 1 && v > -2 && v < P->hf_l + 1)) return 0;
-    double reach = r + P->contact_thresh;
+    real reach = r + P->contact_thresh;
     int i0 = (int)floor(u - reach / P->hf_s[0]), i1 = (int)floor(u + reach / P->hf_s[0]);
     int j0 = (int)floor(v - reach / P->hf_s[1]), j1 = (int)floor(v + reach / P->hf_s[1]);
     if (i0 < 0) i0 = 0;
@@ -508,52 +570,52 @@ static int terrain_contact(const om_params* P, const double* c, double r, double
     if (i1 > P->hf_w - 2) i1 = P->hf_w - 2;
     if (j1 > P->hf_l - 2) j1 = P->hf_l - 2;
     if (i0 > i1 || j0 > j1) return 0;
-    double best = -1, q[3] = {0, 0, 0};
+    real best = -1, q[3] = {0, 0, 0};
     for (int cj = j0; cj <= j1; cj++)
         for (int ci = i0; ci <= i1; ci++)
             for (int t = 0; t < 2; t++) {
                 int di[3], dj[3];
-                double va[3], vb[3], vc[3], qq[3], dv[3];
+                real va[3], vb[3], vc[3], qq[3], dv[3];
                 tri_corners(ci, cj, t, di, dj);
                 hf_vertex(P, ci + di[0], cj + dj[0], va);
                 hf_vertex(P, ci + di[1], cj + dj[1], vb);
                 hf_vertex(P, ci + di[2], cj + dj[2], vc);
                 closest_tri(c, va, vb, vc, qq);
                 for (int k = 0; k < 3; k++) dv[k] = c[k] - qq[k];
-                double d2 = dot3(dv, dv);
+                real d2 = dot3(dv, dv);
                 if (best < 0 || d2 < best) { best = d2; memcpy(q, qq, sizeof q); }
             }
-    double nf[3] = {0, 0, 1}, sd = 1;
+    real nf[3] = {0, 0, 1}, sd = 1;
     int fi = (int)floor(u), fj = (int)floor(v);
     if (fi >= 0 && fi <= P->hf_w - 2 && fj >= 0 && fj <= P->hf_l - 2) {
-        double fa = u - fi, fb = v - fj;
+        real fa = u - fi, fb = v - fj;
         int t = !((fi + fj) & 1) ? (fb >= fa ? 0 : 1) : (fa + fb <= 1 ? 0 : 1);
         int di[3], dj[3];
-        double va[3], vb[3], vc[3], e1[3], e2[3], ap[3];
+        real va[3], vb[3], vc[3], e1[3], e2[3], ap[3];
         tri_corners(fi, fj, t, di, dj);
         hf_vertex(P, fi + di[0], fj + dj[0], va);
         hf_vertex(P, fi + di[1], fj + dj[1], vb);
         hf_vertex(P, fi + di[2], fj + dj[2], vc);
         for (int k = 0; k < 3; k++) { e1[k] = vb[k] - va[k]; e2[k] = vc[k] - va[k]; ap[k] = c[k] - va[k]; }
         cross(e1, e2, nf);
-        double il = (nf[2] < 0 ? -1.0 : 1.0) / norm3(nf);
+        real il = (nf[2] < 0 ? -1.0 : 1.0) / norm3(nf);
         for (int k = 0; k < 3; k++) nf[k] *= il;
         sd = dot3(ap, nf);
     }
     if (sd < 0) {
-        memcpy(n, nf, 3 * sizeof(double));
+        memcpy(n, nf, 3 * sizeof(real));
         *d = sd - r;
     } else {
-        double dist = sqrt(best);
-        if (dist <= 1e-9) { memcpy(n, nf, 3 * sizeof(double)); *d = -r; }
+        real dist = sqrt(best);
+        if (dist <= 1e-9) { memcpy(n, nf, 3 * sizeof(real)); *d = -r; }
         else { for (int k = 0; k < 3; k++) n[k] = (c[k] - q[k]) / dist; *d = dist - r; }
     }
     return *d < P->contact_thresh;
 }
 
-static int collide(const om_params* P, const om_kin* K, om_contact* C) {
+static int collide(const rparams* P, const om_kin* K, om_contact* C) {
     int nc = 0;
-    double gp1[OM_NG][3], gp2[OM_NG][3];
+    real gp1[OM_NG][3], gp2[OM_NG][3];
     for (int g = 0; g < OM_NG; g++) {
         link_point(K, om_glink[g], om_gp1 + 3 * g, gp1[g]);
         link_point(K, om_glink[g], om_gp2 + 3 * g, gp2[g]);
@@ -561,9 +623,9 @@ static int collide(const om_params* P, const om_kin* K, om_contact* C) {
     for (int g = 0; g < OM_NG; g++) {
         int ne = om_gtype[g] == 0 ? 1 : 2;
         for (int e = 0; e < ne; e++) {
-            const double* p = e == 0 ? gp1[g] : gp2[g];
+            const real* p = e == 0 ? gp1[g] : gp2[g];
             if (P->terrain) {   /* heightfield ground */
-                double n[3], d;
+                real n[3], d;
                 if (terrain_contact(P, p, om_gr[g], n, &d) && nc < P->max_contacts) {
                     om_contact* c = &C[nc++];
                     c->la = om_glink[g]; c->lb = -1;
@@ -576,7 +638,7 @@ static int collide(const om_params* P, const om_kin* K, om_contact* C) {
                 }
                 continue;
             }
-            double d = p[2] - om_gr[g];
+            real d = p[2] - om_gr[g];
             if (d < P->contact_thresh && nc < P->max_contacts) {
                 om_contact* c = &C[nc++];
                 c->la = om_glink[g]; c->lb = -1;
@@ -590,11 +652,11 @@ static int collide(const om_params* P, const om_kin* K, om_contact* C) {
     if (P->self_collision) {
         for (int k = 0; k < OM_NPAIR; k++) {
             int ga = om_pair_a[k], gb = om_pair_b[k];
-            double ca[3], cb[3], dv[3];
+            real ca[3], cb[3], dv[3];
             seg_seg(gp1[ga], gp2[ga], gp1[gb], gp2[gb], ca, cb);
             for (int i = 0; i < 3; i++) dv[i] = ca[i] - cb[i];
-            double dist = norm3(dv);
-            double d = dist - om_gr[ga] - om_gr[gb];
+            real dist = norm3(dv);
+            real d = dist - om_gr[ga] - om_gr[gb];
             if (d < P->contact_thresh && dist > 1e-9 && nc < P->max_contacts) {
                 om_contact* c = &C[nc++];
                 c->la = om_glink[ga]; c->lb = om_glink[gb];
@@ -610,11 +672,14 @@ static int collide(const om_params* P, const om_kin* K, om_contact* C) {
     return nc;
 }
 
+#ifndef OM_F32
 int om_contacts(const om_params* P, const double* st, double* out /* [MAXC][12] */) {
     om_kin K;
     om_contact C[MAXC];
     fk(st, &K);
-    int nc = collide(P, &K, C);
+    rparams Q;
+    to_rparams(P, &Q);
+    int nc = collide(&Q, &K, C);
     for (int i = 0; i < nc; i++) {
         double* o = out + 12 * i;
         o[0] = C[i].la; o[1] = C[i].lb; o[2] = C[i].d; o[3] = C[i].mu;
@@ -623,14 +688,15 @@ int om_contacts(const om_params* P, const double* st, double* out /* [MAXC][12] 
     }
     return nc;
 }
+#endif
 
-static void plane_space(const double* n, double* p, double* q) { /* btPlaneSpace1 */
+static void plane_space(const real* n, real* p, real* q) { /* btPlaneSpace1 */
     if (fabs(n[2]) > 0.7071067811865475244) {
-        double a = n[1] * n[1] + n[2] * n[2], k = 1.0 / sqrt(a);
+        real a = n[1] * n[1] + n[2] * n[2], k = 1.0 / sqrt(a);
         p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
         q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
     } else {
-        double a = n[0] * n[0] + n[1] * n[1], k = 1.0 / sqrt(a);
+        real a = n[0] * n[0] + n[1] * n[1], k = 1.0 / sqrt(a);
         p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
         q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
     }
@@ -638,15 +704,15 @@ static void plane_space(const double* n, double* p, double* q) { /* btPlaneSpace
 
 /* --------------------------------------------------------------------------- one substep */
 typedef struct {
-    double J[NV], MiJ[NV];
-    double meff, b, lo, hi, lam;
+    real J[NV], MiJ[NV];
+    real meff, b, lo, hi, lam;
     int kind;  /* 0 limit, 1 normal, 2 friction */
     int normal_row;
-    double mu;
+    real mu;
 } om_row;
 
-static void substep(const om_params* P, double* st, const double* tau, int* ncontact_out) {
-    const double dt = P->dt;
+static void substep(const rparams* P, real* st, const real* tau, int* ncontact_out) {
+    const real dt = P->dt;
     om_kin K;
     fk(st, &K);
     om_contact C[MAXC];
@@ -654,7 +720,7 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
     if (ncontact_out) *ncontact_out = nc;
 
     /* 1. unconstrained dynamics -> nu* */
-    double acc[NV], nu[NV];
+    real acc[NV], nu[NV];
     aba(P, st, &K, tau, acc);
     for (int i = 0; i < 3; i++) { nu[i] = st[10 + i] + dt * acc[i]; nu[3 + i] = st[7 + i] + dt * acc[3 + i]; }
     for (int j = 0; j < OM_ND; j++) nu[6 + j] = st[30 + j] + dt * acc[6 + j];
@@ -663,15 +729,15 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
     /* 2. constraint rows */
     om_row rows[MAXROW];   /* on the stack: the OpenMP batch driver steps lanes concurrently */
     int nr = 0;
-    double H[NV * NV];
+    real H[NV * NV];
     mass_matrix(&K, H);
     if (P->joint_damping)   /* constraint responses see the same implicit-damping inertia as the ABA */
         for (int j = 0; j < OM_ND; j++) H[(6 + j) * NV + 6 + j] += dt * om_jdamp[j];
     cholesky(H, NV);
     for (int j = 0; j < OM_ND; j++) {  /* joint limits: lower then upper */
-        double q = st[13 + j];
+        real q = st[13 + j];
         for (int side = 0; side < 2; side++) {
-            double pen = side == 0 ? q - om_lo[j] : om_hi[j] - q;
+            real pen = side == 0 ? q - om_lo[j] : om_hi[j] - q;
             if (pen > 0) continue;
             om_row* r = &rows[nr++];
             memset(r->J, 0, sizeof r->J);
@@ -681,7 +747,7 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
         }
     }
     int first_normal = nr;
-    double Jp[3 * NV], Jq[3 * NV];
+    real Jp[3 * NV], Jq[3 * NV];
     for (int k = 0; k < nc; k++) {
         om_contact* c = &C[k];
         point_jacobian(&K, c->la, c->pa, Jp);
@@ -703,21 +769,21 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
             point_jacobian(&K, c->lb, c->pb, Jq);
             for (int i = 0; i < 3 * NV; i++) Jp[i] -= Jq[i];
         }
-        double vrel[3] = {0, 0, 0};
+        real vrel[3] = {0, 0, 0};
         for (int i = 0; i < 3; i++)
             for (int a = 0; a < NV; a++) vrel[i] += Jp[i * NV + a] * nu[a];
-        double vn = dot3(vrel, c->n), lat[3], t1[3], t2[3];
+        real vn = dot3(vrel, c->n), lat[3], t1[3], t2[3];
         for (int i = 0; i < 3; i++) lat[i] = vrel[i] - c->n[i] * vn;
-        double l2 = dot3(lat, lat);
+        real l2 = dot3(lat, lat);
         if (l2 > 1e-12) {
-            double il = 1.0 / sqrt(l2);
+            real il = 1.0 / sqrt(l2);
             for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
             cross(t1, c->n, t2);
         } else {
             plane_space(c->n, t1, t2);
         }
         for (int f = 0; f < 2; f++) {
-            const double* t = f == 0 ? t1 : t2;
+            const real* t = f == 0 ? t1 : t2;
             om_row* r = &rows[nr++];
             for (int a = 0; a < NV; a++) r->J[a] = t[0] * Jp[a] + t[1] * Jp[NV + a] + t[2] * Jp[2 * NV + a];
             r->kind = 2; r->b = 0; r->mu = c->mu; r->normal_row = first_normal + k;
@@ -728,7 +794,7 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
     for (int i = 0; i < nr; i++) {
         memcpy(rows[i].MiJ, rows[i].J, sizeof rows[i].J);
         chol_solve(H, NV, rows[i].MiJ);
-        double s = 0;
+        real s = 0;
         for (int a = 0; a < NV; a++) s += rows[i].J[a] * rows[i].MiJ[a];
         rows[i].meff = 1.0 / s;
         rows[i].lam = 0;
@@ -738,14 +804,14 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
         for (int i = 0; i < nr; i++) {
             om_row* r = &rows[i];
             if (r->kind == 2) {
-                double ln = rows[r->normal_row].lam;
+                real ln = rows[r->normal_row].lam;
                 r->lo = -r->mu * ln;
                 r->hi = r->mu * ln;
             }
-            double Jv = 0;
+            real Jv = 0;
             for (int a = 0; a < NV; a++) Jv += r->J[a] * nu[a];
-            double lnew = clampd(r->lam + r->meff * (r->b - Jv), r->lo, r->hi);
-            double dl = lnew - r->lam;
+            real lnew = clampd(r->lam + r->meff * (r->b - Jv), r->lo, r->hi);
+            real dl = lnew - r->lam;
             r->lam = lnew;
             for (int a = 0; a < NV; a++) nu[a] += r->MiJ[a] * dl;
         }
@@ -754,28 +820,42 @@ static void substep(const om_params* P, double* st, const double* tau, int* ncon
     for (int i = 0; i < 3; i++) { st[10 + i] = nu[i]; st[7 + i] = nu[3 + i]; st[i] += dt * nu[3 + i]; }
     for (int j = 0; j < OM_ND; j++) { st[30 + j] = nu[6 + j]; st[13 + j] += dt * nu[6 + j]; }
     {
-        const double* w = st + 10;
-        double ang = norm3(w), ax[3];
+        const real* w = st + 10;
+        real ang = norm3(w), ax[3];
         if (ang * dt > 0.25 * M_PI) ang = 0.25 * M_PI / dt;   /* ANGULAR_MOTION_THRESHOLD */
         if (ang < 0.001) {
-            double s = 0.5 * dt - dt * dt * dt * 0.020833333333 * ang * ang;
+            real s = 0.5 * dt - dt * dt * dt * 0.020833333333 * ang * ang;
             for (int i = 0; i < 3; i++) ax[i] = w[i] * s;
         } else {
-            double s = sin(0.5 * ang * dt) / ang;
+            real s = sin(0.5 * ang * dt) / ang;
             for (int i = 0; i < 3; i++) ax[i] = w[i] * s;
         }
-        double dw = cos(0.5 * ang * dt);
-        double* q = st + 3; /* x y z w */
-        double nq[4] = {dw * q[0] + ax[0] * q[3] + ax[1] * q[2] - ax[2] * q[1],
+        real dw = cos(0.5 * ang * dt);
+        real* q = st + 3; /* x y z w */
+        real nq[4] = {dw * q[0] + ax[0] * q[3] + ax[1] * q[2] - ax[2] * q[1],
                         dw * q[1] + ax[1] * q[3] + ax[2] * q[0] - ax[0] * q[2],
                         dw * q[2] + ax[2] * q[3] + ax[0] * q[1] - ax[1] * q[0],
                         dw * q[3] - ax[0] * q[0] - ax[1] * q[1] - ax[2] * q[2]};
-        double nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+        real nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
         for (int i = 0; i < 4; i++) q[i] = nq[i] / nn;
     }
 }
 
 /* ------------------------------------------------------------------------- public API */
+#ifdef OM_F32
+/* the float instantiation: one env step in float arithmetic from a double state (rounded to float on entry, the
+   result widened back) */
+void om_step_f32(const om_params* P, double* st, const double* tau_motor, int* ncontact_out);
+void om_step_f32(const om_params* P, double* st, const double* tau_motor, int* ncontact_out) {
+    rparams Q;
+    to_rparams(P, &Q);
+    real s[47], t[OM_ND];
+    for (int i = 0; i < 47; i++) s[i] = (real)st[i];
+    for (int i = 0; i < OM_ND; i++) t[i] = (real)tau_motor[i];
+    for (int k = 0; k < Q.nsub; k++) substep(&Q, s, t, k == Q.nsub - 1 ? ncontact_out : 0);
+    for (int i = 0; i < 47; i++) st[i] = (double)s[i];
+}
+#else
 void om_default_params(om_params* P) {
     P->dt = 0.0165 / 4.0;
     P->nsub = 4;
@@ -805,14 +885,18 @@ void om_default_params(om_params* P) {
 
 /* one env step of physics: state (47) in place; tau_motor[17] in dof order (already 0.41*power*clip(a)). */
 void om_step(const om_params* P, double* st, const double* tau_motor, int* ncontact_out) {
-    for (int s = 0; s < P->nsub; s++) substep(P, st, tau_motor, s == P->nsub - 1 ? ncontact_out : 0);
+    rparams Q;
+    to_rparams(P, &Q);
+    for (int s = 0; s < Q.nsub; s++) substep(&Q, st, tau_motor, s == Q.nsub - 1 ? ncontact_out : 0);
 }
 
 /* diagnostics used by tests: unconstrained accelerations (ABA) and mass-matrix-based accelerations */
 void om_aba(const om_params* P, const double* st, const double* tau, double* acc) {
     om_kin K;
     fk(st, &K);
-    aba(P, st, &K, tau, acc);
+    rparams Q;
+    to_rparams(P, &Q);
+    aba(&Q, st, &K, tau, acc);
 }
 void om_mass_matrix(const double* st, double* H) {
     om_kin K;
@@ -830,5 +914,8 @@ int om_nv(void) { return NV; }
 /* one ground candidate (sphere centre c, radius r) against the heightfield ground: 1 with normal n and signed
    distance d when in contact range (tests) */
 int om_terrain_contact(const om_params* P, const double* c, double r, double* n, double* d) {
-    return terrain_contact(P, c, r, n, d);
+    rparams Q;
+    to_rparams(P, &Q);
+    return terrain_contact(&Q, c, r, n, d);
 }
+#endif

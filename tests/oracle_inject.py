@@ -9,9 +9,10 @@ from ilrl_amd import _native as N
 BK = N.BK
 
 
-def oracle_from_lane(clip, phys, book):
-    """OracleLowLevelEnv whose physics state, bookkeeping and RNG stream are one lane's hum_get_state rows."""
-    return O.OracleLowLevelEnv.from_lane(clip, phys, book, BK)
+def oracle_from_lane(clip, phys, book, phys_precision="fp64"):
+    """OracleLowLevelEnv whose physics state, bookkeeping and RNG stream are one lane's hum_get_state rows
+    (phys_precision "fp32": the oracle's physics in float arithmetic, the fp32 yardstick)."""
+    return O.OracleLowLevelEnv.from_lane(clip, phys, book, BK, phys_precision=phys_precision)
 
 
 def contact_heavy_states(n, min_contacts=17, seed=1):

@@ -57,6 +57,22 @@ def test_config_layout_matches_header(tmp_path):
         assert getattr(N.HumConfig, f).offset == off, f
 
 
+@pytest.mark.parametrize("cname,cls", [("hum_hier_io", "HumHierIO"), ("hum_hier_traj", "HumHierTraj")])
+def test_hier_rollout_struct_layouts_match_header(tmp_path, cname, cls):
+    S = getattr(N, cls)
+    fields = [f[0] for f in S._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "humanoid_env.h"\nint main(void){\n'
+                   'printf("%%zu\\n", sizeof(%s));\n' % cname +
+                   "".join('printf("%%zu\\n", offsetof(%s, %s));\n' % (cname, f) for f in fields) + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)])
+    out = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert out[0] == ctypes.sizeof(S)
+    for f, off in zip(fields, out[1:]):
+        assert getattr(S, f).offset == off, f
+
+
 def test_default_config_values():
     c = N.default_config()
     assert (c.dt_env, c.substeps, c.solver_iters, c.gravity) == (0.0165, 4, 5, 9.8)

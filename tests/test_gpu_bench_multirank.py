@@ -1,9 +1,11 @@
 """Config 4's real benchmark path (BASELINE.json configs[3]: lanes sharded over ranks, trajectory gather to the
-learner rank) end to end on the one-GPU box: bench.py under torch.distributed.run with 2 ranks (both on cuda:0,
-gloo - RCCL needs one GPU per rank; the 8-GPU RCCL/xGMI run is the driver's), 2048 lanes per rank, 8 env
-steps per launch and a gather every 8 env steps.  Rank 0's gathered obs / action / reward / done fragments must
-equal those of ONE 4096-lane handle stepped with the same actions, bit for bit (every lane's RNG stream is keyed by
-its global id)."""
+learner rank) end to end on the one-GPU box: bench.py under torch.distributed.run (every rank on cuda:0, gloo -
+RCCL needs one GPU per rank; the 8-GPU RCCL/xGMI run is the driver's).  Two shapes: 2 ranks x 2048 lanes, 8 env
+steps per launch, a gather every 8 env steps; and config 4's own shape, 8 ranks x 4096 lanes = 32,768 lanes, 32 env
+steps per launch (the bench default) and a gather every 32 env steps.  Rank 0's gathered obs / action / reward /
+done fragments must equal those of ONE handle over all the lanes stepped with the same actions, bit for bit (every
+lane's RNG stream is keyed by its global id); at 32,768 lanes rank 0 keeps every 61st lane of the
+fragment (all eight shards are sampled) to bound host memory."""
 import json
 import os
 import socket
@@ -22,7 +24,6 @@ if not torch.cuda.is_available():
 from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LANES, K, EVERY, STEPS = 2048, 8, 8, 16
 
 
 def _port():
@@ -33,30 +34,45 @@ def _port():
     return p
 
 
-@pytest.mark.timeout(300)
-def test_bench_two_ranks_gather_equals_single_handle(tmp_path):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("ranks,lanes,k,every,steps,stride", [(2, 2048, 8, 8, 16, 1), (8, 4096, 32, 32, 32, 61)],
+                         ids=["2x2048", "config4_8x4096"])
+def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride):
+    import types
+    sys.path.insert(0, REPO)
+    import bench
     dump = str(tmp_path / "gather.npz")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
-           "--backend", "gloo", "--lanes", str(LANES), "--steps", str(STEPS), "--warmup", "0", "--k", str(K),
-           "--gather-every", str(EVERY), "--dump-gather", dump, "--cpu-seconds", "0"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(ranks),
+           "--backend", "gloo", "--lanes", str(lanes), "--steps", str(steps), "--warmup", "0", "--k", str(k),
+           "--gather-every", str(every), "--dump-gather", dump, "--dump-lane-stride", str(stride), "--cpu-seconds", "0"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
-    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=280, env=env)
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=560, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["config"]["steps_per_launch"] == K
-    assert line["gather"]["every"] == EVERY and line["gather"]["fragments"] == STEPS // EVERY
+    print("bench line:", json.dumps({x: line[x] for x in ("value", "ms_per_step", "n_gpus", "gather")}))
+    assert line["n_gpus"] == ranks and line["config"]["steps_per_launch"] == [k]
+    assert line["config"]["launches"] == steps // k
+    assert line["gather"]["every"] == every and line["gather"]["fragments"] == steps // every
     assert line["value"] > 0 and line["error_flags"] == 0
     g = np.load(dump)
-    one = HumanoidVecEnv(2 * LANES, clips=("motion02_04",), seed=0)
+    total = ranks * lanes
+    sel = np.arange(0, total, stride)
+    assert len(np.unique(sel // lanes)) == ranks   # every shard sampled
+    # the bench's own device-resident action blocks of every rank (bench._pools, seeded by rank), lanes in rank order
+    dev = torch.device("cuda", 0)
+    pools = [bench._pools(types.SimpleNamespace(hier=False), dev, lanes, k, rr)[0] for rr in range(ranks)]
+    one = HumanoidVecEnv(total, clips=("motion02_04",), seed=0)
     one.reset()
-    for j in range(STEPS // EVERY):
-        acts = g["act_%d" % j]   # [lanes, EVERY, 17] lane-major, rank 0's lanes first
-        assert acts.shape == (2 * LANES, EVERY, 17)
-        for t in range(EVERY):
-            obs, rew, done, _ = one.step(torch.as_tensor(np.ascontiguousarray(acts[:, t]), device="cuda"),
-                                         autoreset=True)
-            np.testing.assert_array_equal(obs.cpu().numpy(), g["obs_%d" % j][:, t])
-            np.testing.assert_array_equal(rew.cpu().numpy(), g["reward_%d" % j][:, t])
-            np.testing.assert_array_equal(done.cpu().numpy(), g["done_%d" % j][:, t])
+    for j in range(steps // every):
+        acts = g["act_%d" % j]   # [sampled lanes, every, 17] lane-major, rank 0's lanes first
+        assert acts.shape == (len(sel), every, 17)
+        for s in range(every // k):
+            blk = torch.cat([p[(j * (every // k) + s) % 16] for p in pools], dim=1).contiguous()   # [k, total, 17]
+            np.testing.assert_array_equal(blk[:, sel].transpose(0, 1).cpu().numpy(), acts[:, s * k:(s + 1) * k])
+            obs, rew, done, _, _ = one.step_k(blk, autoreset=True)
+            sl = slice(s * k, (s + 1) * k)
+            np.testing.assert_array_equal(obs[:, sel].transpose(0, 1).cpu().numpy(), g["obs_%d" % j][:, sl])
+            np.testing.assert_array_equal(rew[:, sel].transpose(0, 1).cpu().numpy(), g["reward_%d" % j][:, sl])
+            np.testing.assert_array_equal(done[:, sel].transpose(0, 1).cpu().numpy(), g["done_%d" % j][:, sl])
     one.close()

@@ -221,6 +221,14 @@ def test_check_finite_returns_error_status():
     rc = N.lib().hum_step(env.h, _p(a), _p(obs), _p(rew), _p(done), None,
                           N.HUM_STEP_HOST_IO | N.HUM_STEP_CHECK_FINITE, None, None)
     assert rc == N.HUM_OK
+    # a non-finite action of an earlier UNCHECKED step leaves the sticky bit set; a later checked call whose own
+    # actions are finite still succeeds (the bit is cleared on the stream before its launch)
+    a[5, 0] = np.inf
+    assert N.lib().hum_step(env.h, _p(a), _p(obs), _p(rew), _p(done), None, N.HUM_STEP_HOST_IO, None, None) == N.HUM_OK
+    assert env.error_flags() & N.HUM_EFLAG_NONFINITE_ACTION
+    a[5, 0] = 0.25
+    assert N.lib().hum_step(env.h, _p(a), _p(obs), _p(rew), _p(done), None,
+                            N.HUM_STEP_HOST_IO | N.HUM_STEP_CHECK_FINITE, None, None) == N.HUM_OK
     g = torch.zeros(n, 17, device="cuda")
     assert N.lib().hum_step_graph(env.h, _p(g), _p(env.obs), _p(env.reward), _p(env.done), None,
                                   N.HUM_STEP_CHECK_FINITE, None, 2) == N.HUM_ERR_ARG

@@ -13,7 +13,8 @@ if not torch.cuda.is_available():
     pytest.skip("needs a HIP device", allow_module_level=True)
 
 from ilrl_amd import _native as N  # noqa: E402
-from ilrl_amd.policy import DevicePolicy, reference_mean  # noqa: E402
+from ilrl_amd.hier_env import HierVecEnv  # noqa: E402
+from ilrl_amd.policy import DevicePolicy, hier_rollout, reference_mean  # noqa: E402
 from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
 
@@ -93,40 +94,140 @@ def test_fused_rollout_equals_policy_kernel_and_step_k(k):
     """hum_rollout_fused (the policy inside the multi-step env kernel) vs its two halves run separately: every
     recorded sample equals the standalone policy kernel's on the recorded input (the same k-ordered fp32 fma
     chains), and replaying the clipped samples through hum_step_k from the same start state reproduces the recorded
-    rewards, dones, next inputs and final state bitwise."""
+    rewards, dones, next inputs and final state bitwise.  Both auto-reset paths of the fused kernel run: both envs
+    are first stepped identically until some lanes end done, so the first fused step takes the reset observation
+    of those lanes (done_in set), and with k = 16 lanes also finish inside the launch (their reset observation is
+    read back from LDS at the next step); a second fused rollout continues from the first one's done flags."""
     n = 512
     pol = DevicePolicy.random_init(seed=9)
     envs = [HumanoidVecEnv(n, clips=("motion02_04",), seed=2) for _ in range(2)]
+    g = torch.Generator(device="cuda").manual_seed(3)
+    pre = [torch.rand(n, 17, device="cuda", generator=g) * 2 - 1 for _ in range(40)]
     for e in envs:
         e.done.fill_(1)
         e.reset()
-    tr = pol.rollout(envs[0], k, explore=True, step0=100, fused=True)
-    act = torch.empty(n, 17, device="cuda")
-    raw = torch.empty(n, 17, device="cuda")
-    worst = 0.0
-    for t in range(k):
-        pol.act(tr["obs"][t], explore=True, step=100 + t, out=act, raw_out=raw)
-        worst = max(worst, (tr["actions"][t] - raw).abs().max().item())
-    print("fused policy vs policy kernel: max |sample diff| %.3g" % worst)
-    assert worst == 0.0
-    torch.testing.assert_close(envs[0]._act_buf, tr["actions"][k - 1].clamp(-1, 1), atol=0, rtol=0)
+        for t in range(40):
+            e.step(pre[t], autoreset=True)
+    assert envs[0].done.any(), "no lane ends the warm-up done: the done_in path would not run"
+    done_inside = False
     e = envs[1]
-    obs_k, rew_k, done_k, _, rst_k = e.step_k(tr["actions"].clamp(-1, 1).contiguous(), autoreset=True)
-    torch.testing.assert_close(tr["rewards"], rew_k, atol=0, rtol=0)
-    assert torch.equal(tr["dones"], done_k)
-    for t in range(k - 1):
-        want = torch.where(done_k[t].bool()[:, None], rst_k[t], obs_k[t])
-        torch.testing.assert_close(tr["obs"][t + 1], want, atol=0, rtol=0)
-    torch.testing.assert_close(envs[0].obs, obs_k[k - 1], atol=0, rtol=0)
-    torch.testing.assert_close(envs[0].reward, rew_k[k - 1], atol=0, rtol=0)
-    assert torch.equal(envs[0].done, done_k[k - 1])
-    p0, b0 = envs[0].get_state()
-    p1, b1 = e.get_state()
-    np.testing.assert_array_equal(p0, p1)
-    np.testing.assert_array_equal(b0, b1)
+    want0 = torch.where(e.done.bool()[:, None], e.obs_reset, e.obs).clone()
+    for rnd in range(2):
+        tr = pol.rollout(envs[0], k, explore=True, step0=100 + rnd * k, fused=True)
+        torch.testing.assert_close(tr["obs"][0], want0, atol=0, rtol=0)   # done_in lanes took their reset obs
+        act = torch.empty(n, 17, device="cuda")
+        raw = torch.empty(n, 17, device="cuda")
+        worst = 0.0
+        for t in range(k):
+            pol.act(tr["obs"][t], explore=True, step=100 + rnd * k + t, out=act, raw_out=raw)
+            worst = max(worst, (tr["actions"][t] - raw).abs().max().item())
+        print("fused policy vs policy kernel (round %d): max |sample diff| %.3g" % (rnd, worst))
+        assert worst == 0.0
+        torch.testing.assert_close(envs[0]._act_buf, tr["actions"][k - 1].clamp(-1, 1), atol=0, rtol=0)
+        obs_k, rew_k, done_k, _, rst_k = e.step_k(tr["actions"].clamp(-1, 1).contiguous(), autoreset=True)
+        torch.testing.assert_close(tr["rewards"], rew_k, atol=0, rtol=0)
+        assert torch.equal(tr["dones"], done_k)
+        done_inside |= bool(done_k[:-1].any())
+        for t in range(k - 1):
+            want = torch.where(done_k[t].bool()[:, None], rst_k[t], obs_k[t])
+            torch.testing.assert_close(tr["obs"][t + 1], want, atol=0, rtol=0)
+        torch.testing.assert_close(envs[0].obs, obs_k[k - 1], atol=0, rtol=0)
+        torch.testing.assert_close(envs[0].reward, rew_k[k - 1], atol=0, rtol=0)
+        assert torch.equal(envs[0].done, done_k[k - 1])
+        # the reset observation of lanes done at the launch's last step (the next launch's done_in input)
+        last = done_k[k - 1].bool()
+        torch.testing.assert_close(envs[0].obs_reset[last], rst_k[k - 1][last], atol=0, rtol=0)
+        want0 = torch.where(last[:, None], rst_k[k - 1], obs_k[k - 1]).clone()
+        p0, b0 = envs[0].get_state()
+        p1, b1 = e.get_state()
+        np.testing.assert_array_equal(p0, p1)
+        np.testing.assert_array_equal(b0, b1)
+    if k > 1:
+        assert done_inside, "no lane finished inside a launch: the in-launch reset path did not run"
     for x in envs:
         x.close()
     pol.close()
+
+
+@pytest.mark.parametrize("n_in,n_out", [(44, 2), (70, 17), (5, 32)])
+def test_policy_shapes_match_torch_fp32(n_in, n_out):
+    """hum_policy_create_ex: the same network at other widths (44 -> 2 = the high-level policy)."""
+    pol = DevicePolicy.random_init(seed=4, n_in=n_in, n_out=n_out)
+    pol.w["b3"][:] = np.linspace(-0.2, 0.2, n_out)
+    pol.close()
+    pol = DevicePolicy(pol.w, seed=4, n_in=n_in, n_out=n_out)
+    obs = torch.randn(300, n_in, device="cuda", generator=torch.Generator(device="cuda").manual_seed(2)) * 2
+    mean = torch.empty(300, n_out, device="cuda")
+    act = pol.act(obs, mean_out=mean)
+    ref = reference_mean(pol.w, obs)
+    assert (mean - ref).abs().max().item() < 2e-5
+    torch.testing.assert_close(act, ref.clamp(-1, 1), atol=2e-5, rtol=0)
+    with pytest.raises(ValueError):
+        pol.act(torch.zeros(4, n_in + 1, device="cuda"))
+    pol.close()
+
+
+def test_hier_rollout_equals_python_loop():
+    """hum_hier_rollout (config 5's two-level sampler: high policy, low policy, hum_hier_step with auto-reset per
+    transition) == the same loop driven from Python through hum_policy_act + hum_hier_step, bitwise: policy inputs
+    (done lanes: their auto-reset high observation), raw samples, the agent that acted, returned agents, both
+    rewards, done and the final state.  Two calls in a row: the second starts from the first one's done flags."""
+    n, k = 512, 20
+    high = DevicePolicy.random_init_high(seed=11)
+    low = DevicePolicy.random_init(seed=9)
+    envs = [HierVecEnv(n, seed=4) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    e = envs[1]
+    ah, rah = torch.empty(n, 2, device="cuda"), torch.empty(n, 2, device="cuda")
+    al, ral = torch.empty(n, 17, device="cuda"), torch.empty(n, 17, device="cuda")
+    expect_high = torch.ones(n, dtype=torch.bool, device="cuda")   # after reset every lane's next agent is the high one
+    seen = torch.zeros(3, dtype=torch.int64)
+    for rnd in range(2):
+        tr = hier_rollout(envs[0], high, low, k, explore=True, step0=50 + rnd * k)
+        for t in range(k):
+            step = 50 + rnd * k + t
+            torch.testing.assert_close(tr["obs_high"][t], torch.where(e.done.bool()[:, None], e.obs_high_reset,
+                                                                      e.obs_high), atol=0, rtol=0)
+            torch.testing.assert_close(tr["obs_low"][t], e.obs, atol=0, rtol=0)
+            high.act(e.obs_high, e.obs_high_reset, e.done, explore=True, step=step, out=ah, raw_out=rah)
+            low.act(e.obs, explore=True, step=step, out=al, raw_out=ral)
+            torch.testing.assert_close(tr["act_high"][t], rah, atol=0, rtol=0)
+            torch.testing.assert_close(tr["act_low"][t], ral, atol=0, rtol=0)
+            want = torch.where(expect_high, N.HUM_AGENT_HIGH, N.HUM_AGENT_LOW).to(torch.uint8)
+            assert torch.equal(tr["acted"][t], want)
+            agents, _, _, rh, rl, done, _ = e.step(ah, al, autoreset=True)
+            assert torch.equal(tr["agents"][t], agents) and torch.equal(tr["done"][t], done)
+            torch.testing.assert_close(tr["rew_high"][t], rh, atol=0, rtol=0)
+            torch.testing.assert_close(tr["rew_low"][t], rl, atol=0, rtol=0)
+            expect_high = ((agents & N.HUM_AGENT_HIGH) != 0) | (done != 0)
+            seen += torch.stack([(tr["acted"][t] == N.HUM_AGENT_HIGH).sum(), (tr["acted"][t] == N.HUM_AGENT_LOW).sum(),
+                                 done.sum()]).cpu()
+        for name in ("obs_high", "obs_high_reset", "obs", "done", "agents", "reward_high", "reward"):
+            a0, a1 = getattr(envs[0], name), getattr(e, name)
+            if name == "obs_high_reset":   # rows of lanes that reset at the last transition
+                m = e.done.bool()
+                a0, a1 = a0[m], a1[m]
+            torch.testing.assert_close(a0, a1, atol=0, rtol=0, msg=name)
+        p0, b0 = envs[0].get_state()
+        p1, b1 = e.get_state()
+        np.testing.assert_array_equal(p0, p1)
+        np.testing.assert_array_equal(b0, b1)
+    assert (seen > 0).all(), "high and low transitions and auto-resets must all occur: %s" % seen.tolist()
+    for x in envs:
+        x.close()
+    high.close()
+    low.close()
+
+
+def test_hier_rollout_rejects_wrong_shapes():
+    env = HierVecEnv(64, seed=1)
+    env.reset()
+    low = DevicePolicy.random_init(seed=1)
+    with pytest.raises(N.NativeError, match="hum_hier_rollout"):
+        hier_rollout(env, low, low, 2)
+    env.close()
+    low.close()
 
 
 def test_fused_rollout_rejects_other_kernels():

@@ -12,8 +12,9 @@
 
 Tolerances: frame, timestep and the RNG counter bit-exact everywhere.  fp64 kernel: state 1e-6 after a full
 step (different but exact formulations), obs 1e-5, reward 1e-5, done exact.  fp32 kernel
-(the benchmarked build) vs the fp64 oracle over ONE step from the identical state: see FP32_BOUND and SENS_BOUND
-below.
+(the benchmarked build) vs the fp64 oracle over ONE step from the identical state, held to the error of the
+oracle's own physics run in float arithmetic from that state (the fp32 yardstick): see FP32_FLOOR / FP32_RATIO
+and SENS_BOUND below.  A k = 32 variant steps the benchmark's launch shape (hum_step_k, 4096 lanes).
 """
 import json
 import os
@@ -35,11 +36,25 @@ from ilrl_amd import _native as N  # noqa: E402
 from ilrl_amd.clips import CLIP_NAMES, load_clip  # noqa: E402
 from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
-# one fp32 env step vs the fp64 oracle from the same state ("fp32 step bound"): float32
-# rounding through 4 substeps of dynamics and the contact / limit solve; measured over the sampled lanes (obs
-# max 3.4e-5 - 5.1e-5 conditioned, reward max 1.7e-6, no done flips; profiles/r02_parity_scale_*.json,
-# profiles/r03_*), bound 2x the worst measured
+# one fp32 env step vs the fp64 oracle from the same state ("fp32 step bound").  The yardstick
+# is the oracle's own physics instantiated in float arithmetic (oracle/physics_oracle_f32.c) stepped from the same
+# state: its distance from the fp64 oracle is the rounding error intrinsic to an fp32 step of this algorithm
+# (measured: 3e-5 - 8e-5 in the joint speeds, above SURVEY's 1e-5 - no fp32 step of this physics meets 1e-5).  The
+# envelope is that error's max over FP32_REALISATIONS fp32-oracle steps per lane: from the lane's state and from the
+# state perturbed by 2^-24 relative (one float32 rounding of the input, which an fp32 step cannot resolve).  On the
+# well-conditioned lanes the kernel must stay, per obs block (the 8 body terms, the 17 joint positions, the 17 joint
+# speeds) and for the reward, within max(FP32_FLOOR, FP32_RATIO x the envelope's max), and its median over the lanes
+# within 2 x the unperturbed fp32 oracle's median (the max of a few dozen heavy-tailed draws is noisy, the median is
+# not); the 28 clip-table values differ only by their float32 output rounding (<= FP32_FLOOR).  Over ALL lanes
+# (ill-conditioned ones included) the reward stays within max(1e-4, 2 x the envelope's).
+FP32_FLOOR = {"obs": 1e-5, "reward": 1e-5}
+FP32_RATIO = 1.5
+FP32_REALISATIONS = 4
+# the fixed bound the short-scenario tests (the hier golden scenarios, terrain) still use: 2x round 2's worst
+# measured conditioned error
 FP32_BOUND = {"obs_max": 1e-4, "reward_max": 1e-5}
+OBS_BLOCKS = {"body": np.arange(0, 8), "joint_pos": np.arange(8, 42, 2), "joint_vel": np.arange(9, 42, 2),
+              "clip_table": np.arange(42, 70)}
 # Conditioning: a lane whose oracle step moves its obs by more than SENS_BOUND when the input state is perturbed by
 # 2^-24 relative (float32 rounding) sits at a discontinuity of the model (a joint limit or contact switching on within
 # that margin; Bullet's limits and contacts act only when violated / within the threshold).  There float32 vs float64
@@ -71,17 +86,30 @@ def _sample_lanes(book, c, name, per_clip, n):
     return lanes[idx]
 
 
-def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=21):
+def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=21, k=1):
+    """k = 1: the rollout and the compared step are hum_step launches.  k > 1: the bench's launch shape - the rollout
+    runs in hum_step_k launches of k env steps and the compared step is the first row of a k-step launch (its state
+    after that step is not observable, so the state comparison is skipped)."""
     env = HumanoidVecEnv(n, clips=clips, seed=seed, precision=precision)
     env.reset()
     g = torch.Generator(device="cuda").manual_seed(4)
-    for _ in range(steps):
-        env.step(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
+    if k == 1:
+        for _ in range(steps):
+            env.step(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
+    else:
+        for _ in range(steps // k):
+            env.step_k(torch.rand(k, n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
     flags = env.error_flags()
     phys, book = env.get_state()
     a = np.random.default_rng(5).uniform(-1, 1, (n, 17)).astype(np.float32)
-    obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
-    phys2, book2 = env.get_state()
+    if k == 1:
+        obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
+        phys2, book2 = env.get_state()
+    else:
+        ak = torch.rand(k, n, 17, device="cuda", generator=g) * 2 - 1
+        ak[0] = torch.as_tensor(a, device="cuda")
+        obs, rew, done, frame, _ = [x[0].cpu().numpy() for x in env.step_k(ak, autoreset=True)]
+        phys2, book2 = None, None
     env.close()
     # the fp64 kernel from the identical state, base quaternion renormalised (checks the lanes the fp32 bound
     # excludes; see unit_quat)
@@ -93,17 +121,33 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
     phys64, _ = env64.get_state()
     env64.close()
     st = {"obs": [], "rew": [], "done": [], "state": [], "sens": [], "frame_ok": True, "lanes": 0,
-          "obs64": [], "rew64": [], "done64": [], "state64": []}
+          "obs64": [], "rew64": [], "done64": [], "state64": [], "obs_vec": [], "obs_vec_o32": [], "rew_o32": [],
+          "obs_vec_o32env": [], "rew_o32env": []}
     prng = np.random.default_rng(6)
+    prng32 = np.random.default_rng(7)
     for c, name in enumerate(clips):
         clip = load_clip(name)
         for i in _sample_lanes(book, c, name, per_clip, n):
             o = oracle_from_lane(clip, phys[i], book[i])
             ro, rr, rd, _ = o.step(a[i])
             st["obs"].append(np.abs(obs[i] - ro).max())
+            st["obs_vec"].append(np.abs(obs[i] - ro))
             st["rew"].append(abs(float(rew[i]) - rr))
             st["done"].append(bool(done[i]) != rd)
-            st["state"].append(np.abs(phys2[i] - o.state).max())
+            if phys2 is not None:
+                st["state"].append(np.abs(phys2[i] - o.state).max())
+            # the fp32 yardstick: the oracle's physics in float arithmetic from the same state (realisation 0) and
+            # from the state perturbed by one float32 rounding (the envelope)
+            env_o, env_r = np.zeros(70), 0.0
+            for rz in range(FP32_REALISATIONS):
+                pst = phys[i] if rz == 0 else phys[i] * (1 + 2.0 ** -24 * prng32.choice([-1.0, 1.0], 47))
+                r32o, r32r, _, _ = oracle_from_lane(clip, pst, book[i], phys_precision="fp32").step(a[i])
+                if rz == 0:
+                    st["obs_vec_o32"].append(np.abs(r32o - ro))
+                    st["rew_o32"].append(abs(r32r - rr))
+                env_o, env_r = np.maximum(env_o, np.abs(r32o - ro)), max(env_r, abs(r32r - rr))
+            st["obs_vec_o32env"].append(env_o)
+            st["rew_o32env"].append(env_r)
             o64 = oracle_from_lane(clip, physn[i], book[i])
             ro64, rr64, rd64, _ = o64.step(a[i])
             st["obs64"].append(np.abs(obs64[i] - ro64).max())
@@ -112,8 +156,10 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
             st["state64"].append(np.abs(phys64[i] - o64.state).max())
             p = oracle_from_lane(clip, phys[i] * (1 + 2.0 ** -24 * prng.choice([-1.0, 1.0], 47)), book[i])
             st["sens"].append(np.abs(p.step(a[i])[0] - ro).max())
-            st["frame_ok"] &= int(frame[i]) == o.frame and int(book2[i, BK["cur_timestep"]]) == o.cur_timestep
-            st["frame_ok"] &= int(book2[i, BK["rng_counter"]]) == o.rng.counter
+            st["frame_ok"] &= int(frame[i]) == o.frame
+            if book2 is not None:
+                st["frame_ok"] &= int(book2[i, BK["cur_timestep"]]) == o.cur_timestep
+                st["frame_ok"] &= int(book2[i, BK["rng_counter"]]) == o.rng.counter
             st["lanes"] += 1
     return flags, {k: (np.array(v) if isinstance(v, list) else v) for k, v in st.items()}
 
@@ -123,7 +169,8 @@ def _summary(tag, st):
     s = {"lanes": st["lanes"], "obs_max": float(st["obs"].max()), "obs_p99": float(np.percentile(st["obs"], 99)),
          "obs_p50": float(np.median(st["obs"])), "reward_max": float(st["rew"].max()),
          "reward_p99": float(np.percentile(st["rew"], 99)), "done_mismatch": int(st["done"].sum()),
-         "state_max": float(st["state"].max()), "state_p50": float(np.median(st["state"])),
+         "state_max": float(st["state"].max()) if len(st["state"]) else None,
+         "state_p50": float(np.median(st["state"])) if len(st["state"]) else None,
          "ill_conditioned": int((~good).sum()), "obs_max_conditioned": float(st["obs"][good].max()),
          "reward_max_conditioned": float(st["rew"][good].max()),
          "done_mismatch_conditioned": int(st["done"][good].sum()), "sens_max": float(st["sens"].max())}
@@ -131,6 +178,26 @@ def _summary(tag, st):
         s["fp64_kernel_same_state"] = {"obs_max": float(st["obs64"].max()), "reward_max": float(st["rew64"].max()),
                                        "state_max": float(st["state64"].max()), "done_mismatch": int(st["done64"].sum()),
                                        "obs_max_ill_conditioned": float(st["obs64"][~good].max(initial=0))}
+    if len(st.get("obs_vec_o32", [])):
+        # per obs component and block, well-conditioned lanes: the kernel vs the fp32 oracle (both vs the fp64 oracle)
+        kv, ov, ev = st["obs_vec"][good], st["obs_vec_o32"][good], st["obs_vec_o32env"][good]
+        rms = lambda x: float(np.sqrt(np.mean(np.square(x)))) if len(x) else 0.0
+        s["fp32_oracle"] = {
+            "obs_max_conditioned": float(ov.max()), "reward_max_conditioned": float(st["rew_o32"][good].max()),
+            "obs_max": float(st["obs_vec_o32"].max()), "reward_max": float(st["rew_o32"].max()),
+            "envelope": {"realisations": FP32_REALISATIONS, "obs_max_conditioned": float(ev.max()),
+                         "reward_max_conditioned": float(st["rew_o32env"][good].max()),
+                         "reward_max": float(st["rew_o32env"].max())},
+            "reward_rms_conditioned": {"kernel": rms(st["rew"][good]), "fp32_oracle": rms(st["rew_o32"][good])},
+            "blocks": {b: {"kernel": float(kv[:, ix].max()), "fp32_oracle": float(ov[:, ix].max()),
+                           "fp32_envelope": float(ev[:, ix].max()), "kernel_rms": rms(kv[:, ix].max(1)),
+                           "fp32_oracle_rms": rms(ov[:, ix].max(1)), "kernel_p50": float(np.median(kv[:, ix].max(1))),
+                           "fp32_oracle_p50": float(np.median(ov[:, ix].max(1))),
+                           "lanes_kernel": [float(x) for x in kv[:, ix].max(1)],
+                           "lanes_fp32_oracle": [float(x) for x in ov[:, ix].max(1)]}
+                       for b, ix in OBS_BLOCKS.items()},
+            "per_component": {"kernel": [float(x) for x in kv.max(0)], "fp32_oracle": [float(x) for x in ov.max(0)],
+                              "fp32_envelope": [float(x) for x in ev.max(0)]}}
     print(tag, json.dumps(s))
     out = os.environ.get("ILRL_PARITY_OUT")
     if out:
@@ -139,16 +206,17 @@ def _summary(tag, st):
     return s
 
 
-@pytest.mark.parametrize("config", ["c2", "c3"])
-@pytest.mark.parametrize("precision", ["fp32", "fp64"])
-def test_full_size_rollout_no_drop_and_sample_matches_oracle(config, precision):
+@pytest.mark.parametrize("config,precision,k", [("c2", "fp32", 1), ("c2", "fp64", 1), ("c3", "fp32", 1),
+                                               ("c3", "fp64", 1), ("c2", "fp32", 32)])
+def test_full_size_rollout_no_drop_and_sample_matches_oracle(config, precision, k):
+    """k = 32: the benchmark's launch shape (4096 lanes, 32 env steps per hum_step_k launch)."""
     clips = ("motion02_04",) if config == "c2" else tuple(CLIP_NAMES)
-    flags, st = rollout_and_compare(clips, precision)
+    flags, st = rollout_and_compare(clips, precision, steps=192 if k > 1 else 200, k=k)
     assert flags & N.HUM_EFLAG_CONTACT_OVERFLOW == 0, "a contact was dropped"
     assert flags & N.HUM_EFLAG_NONFINITE_ACTION == 0
     assert st["lanes"] >= 64 * len(clips) - (64 if config == "c3" else 0)
     assert st["frame_ok"], "frame / timestep / RNG counter differ from the oracle"
-    s = _summary("%s_%s" % (config, precision), st)
+    s = _summary("%s_%s%s" % (config, precision, "_k%d" % k if k > 1 else ""), st)
     if precision == "fp64":
         assert s["state_max"] < 1e-6
         assert s["obs_max"] < 1e-5 and s["reward_max"] < 1e-5
@@ -158,8 +226,17 @@ def test_full_size_rollout_no_drop_and_sample_matches_oracle(config, precision):
 
 
 def _check_fp32(s):
-    assert s["obs_max_conditioned"] <= FP32_BOUND["obs_max"]
-    assert s["reward_max_conditioned"] <= FP32_BOUND["reward_max"]
+    o32 = s.get("fp32_oracle")
+    if o32 is not None:   # per obs block and the reward, against the fp32 yardstick
+        for b, v in o32["blocks"].items():
+            if b == "clip_table":   # float32 output rounding of the float64 table values only
+                assert v["kernel"] <= FP32_FLOOR["obs"], (b, v)
+                continue
+            assert v["kernel"] <= max(FP32_FLOOR["obs"], FP32_RATIO * v["fp32_envelope"]), (b, v)
+            assert v["kernel_p50"] <= max(1e-7, 2 * v["fp32_oracle_p50"]), (b, v)
+        env = o32["envelope"]
+        assert s["reward_max_conditioned"] <= max(FP32_FLOOR["reward"], FP32_RATIO * env["reward_max_conditioned"])
+        assert s["reward_max"] <= max(1e-4, 2 * env["reward_max"]), (s["reward_max"], env)
     assert s["done_mismatch_conditioned"] == 0
     assert s["ill_conditioned"] <= MAX_ILL_FRACTION * s["lanes"]
     f64 = s["fp64_kernel_same_state"]   # every lane incl. the excluded ones: the model, not the kernel
@@ -231,9 +308,11 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
     agents, oh, ol, rh, rl, done, frame, phys2, book2 = outs[precision]
     a64, oh64, ol64, rh64, rl64, d64, _, p64, _ = outs["f64"]
     expect = book[:, BK["expect_high"]].astype(int)
-    st = {k: [] for k in ("obs", "rew", "done", "state", "sens", "obs64", "rew64", "done64", "state64", "kind")}
+    st = {k: [] for k in ("obs", "rew", "done", "state", "sens", "obs64", "rew64", "done64", "state64", "kind",
+                          "obs_vec", "obs_vec_o32", "rew_o32", "obs_vec_o32env", "rew_o32env")}
     st["exact_ok"], st["lanes"] = True, 0
     prng = np.random.default_rng(16)
+    prng32 = np.random.default_rng(17)
     for kind in (1, 0):   # high-level transition, low-level (physics) transition
         lanes = np.nonzero(expect == kind)[0]
         assert len(lanes) >= per_kind
@@ -258,6 +337,21 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
                 r = max(abs(float(r_h[i]) - float(rrew.get(OH.HIGH, 0))), abs(float(r_l[i]) - float(rrew.get(OH.LOW, 0))))
                 return e, r
             eo, er = errs(oh, ol, rh, rl, robs, rrew)
+            # per low-obs component, and the fp32 yardstick (the oracle's physics in float arithmetic)
+            lowvec = lambda ob: np.abs(ob - robs[OH.LOW]) if OH.LOW in robs else np.zeros(70)
+            st["obs_vec"].append(lowvec(ol[i]))
+            env_o, env_r = np.zeros(70), 0.0
+            for rz in range(FP32_REALISATIONS):
+                pst = phys[i] if rz == 0 else phys[i] * (1 + 2.0 ** -24 * prng32.choice([-1.0, 1.0], 47))
+                robs32, rrew32, _, _ = OH.OracleHierEnv.from_lane(clip, pst, book[i], BK, phys_precision="fp32").step(act)
+                vo = lowvec(robs32[OH.LOW]) if OH.LOW in robs32 else np.zeros(70)
+                vr = max(abs(float(rrew32.get(a_, 0)) - float(rrew.get(a_, 0))) for a_ in (OH.HIGH, OH.LOW))
+                if rz == 0:
+                    st["obs_vec_o32"].append(vo)
+                    st["rew_o32"].append(vr)
+                env_o, env_r = np.maximum(env_o, vo), max(env_r, vr)
+            st["obs_vec_o32env"].append(env_o)
+            st["rew_o32env"].append(env_r)
             o64 = OH.OracleHierEnv.from_lane(clip, unit_quat(phys[i]), book[i], BK)   # the fp64 cross-check's
             robs64, rrew64, rdone64, _ = o64.step(act)
             eo64, er64 = errs(oh64, ol64, rh64, rl64, robs64, rrew64)

@@ -7,7 +7,7 @@ L=$PWD/imitation-learning-rl_amd/ilrl_amd/_lib
 for rep in 1 2; do
 for n in ${LIBS}; do
   v="EXTRA_$n"
-  ILRL_AMD_LIB=$L/libhumenv_$n.so timeout -k 10 120 python3 bench.py --steps ${STEPS:-1000} --warmup 100 --cpu-seconds 0 --no-secondary ${EXTRA:-} ${!v:-} > gpurun_out/ab_$n.log 2>&1 || { tail -5 gpurun_out/ab_$n.log; exit 1; }
+  ILRL_AMD_AB=1 ILRL_AMD_LIB=$L/libhumenv_$n.so timeout -k 10 120 python3 bench.py --steps ${STEPS:-1000} --warmup 100 --cpu-seconds 0 --no-secondary ${EXTRA:-} ${!v:-} > gpurun_out/ab_$n.log 2>&1 || { tail -5 gpurun_out/ab_$n.log; exit 1; }
   python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_$n.log').read().strip().splitlines()[-1]); print('%-10s %.3fM env-steps/s  kernel %.4f ms  flags %d' % ('$n', d['value']/1e6, d['roofline']['kernel_ms'], d['error_flags']))"
 done
 done
