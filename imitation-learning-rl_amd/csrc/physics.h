@@ -145,16 +145,25 @@ __device__ inline T clampT(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi 
 // (rewards, observations) never uses these.
 template <typename T>
 __device__ inline T prcp(T x) {
+#ifdef HUM_EXACT_MATH   // diagnostics: correctly rounded reciprocal / square roots (the fp32 accuracy study)
+    if constexpr (sizeof(T) == 4) return 1.0f / x;
+#endif
     if constexpr (sizeof(T) == 4) return __builtin_amdgcn_rcpf(x);
     else return T(1) / x;
 }
 template <typename T>
 __device__ inline T psqrt(T x) {
+#ifdef HUM_EXACT_MATH
+    if constexpr (sizeof(T) == 4) return sqrtf(x);
+#endif
     if constexpr (sizeof(T) == 4) return __builtin_amdgcn_sqrtf(x);
     else return sqrt(x);
 }
 template <typename T>
 __device__ inline T prsqrt(T x) {
+#ifdef HUM_EXACT_MATH
+    if constexpr (sizeof(T) == 4) return 1.0f / sqrtf(x);
+#endif
     if constexpr (sizeof(T) == 4) return __builtin_amdgcn_rsqf(x);
     else return T(1) / sqrt(x);
 }

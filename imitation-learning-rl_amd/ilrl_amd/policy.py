@@ -51,8 +51,15 @@ class DevicePolicy:
                 raise ValueError("%s: shape %s, expected %s" % (k, a.shape, shapes[k]))
             self.w[k] = a
         h = ctypes.c_void_p()
-        N.check(N.lib().hum_policy_create_ex(device, n_in, n_out, *[_fp(self.w[k]) for k in self.KEYS],
-                                             ctypes.c_uint64(seed), ctypes.byref(h)), "hum_policy_create")
+        L = N.lib()
+        if callable(L.hum_policy_create_ex):
+            N.check(L.hum_policy_create_ex(device, n_in, n_out, *[_fp(self.w[k]) for k in self.KEYS],
+                                           ctypes.c_uint64(seed), ctypes.byref(h)), "hum_policy_create")
+        else:   # ILRL_AMD_AB: a library older than ABI 10 has only the (70, 17) entry point
+            if (n_in, n_out) != (N.HUM_NOBS, N.HUM_NACT):
+                raise N.NativeError("hum_policy_create_ex missing from %s" % N.LIB_PATH)
+            N.check(L.hum_policy_create(device, *[_fp(self.w[k]) for k in self.KEYS], ctypes.c_uint64(seed),
+                                        ctypes.byref(h)), "hum_policy_create")
         self.h = h
 
     @classmethod
