@@ -16,11 +16,21 @@ L = N.lib()
 L.hum_debug_wave_log.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
 g = torch.Generator(device="cuda").manual_seed(1)
 pool = [(torch.rand(K, n, 17, device="cuda", generator=g) * 2 - 1).contiguous() for _ in range(8)]
-for s in range(10):
-    env.step_k(pool[s % 8], autoreset=True)
+# EARLY=1: the driver's bench shape instead of the steady state - every launch starts from a fresh reset of all lanes
+# (a new seed each time), 5 warm-up env steps in one launch, then the logged launch of K steps (bench.py --steps K
+# --warmup 5)
+EARLY = os.environ.get("EARLY") == "1"
+if not EARLY:
+    for s in range(10):
+        env.step_k(pool[s % 8], autoreset=True)
 rows = []
 buf = np.zeros((nb, 32), np.uint32)
 for s in range(30):
+    if EARLY:
+        env.close()
+        env = HumanoidVecEnv(n, clips=("motion02_04",), seed=100 + s)
+        env.reset()
+        env.step_k(pool[s % 8][:5].contiguous(), autoreset=True)
     L.hum_debug_wave_log(None, nb, 1)
     _, _, done, _ = env.step_k(pool[s % 8], autoreset=True)[:4]
     L.hum_debug_wave_log(buf.ctypes.data, nb, 0)
