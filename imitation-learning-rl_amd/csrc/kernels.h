@@ -332,9 +332,11 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
     float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
 #pragma unroll
     for (int k = 0; k < HUM_NOBS; k++) orow[k] = obs[k];
+    SUBPHASE(16);
     a.rew[io] = (float)total;
     a.done[io] = done ? 1 : 0;
     if (a.frame_out) a.frame_out[io] = b.frame;
+    SUBPHASE(23);
     if (defer_reset) {
         *defer_reset = done && (a.flags & HUM_STEP_AUTORESET);
         return;

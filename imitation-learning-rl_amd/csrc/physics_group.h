@@ -2,7 +2,8 @@
 //
 // MI355X mapping: a 64-lane wavefront = 4 envs x 16 lanes; each env's working set lives in LDS
 // (struct GroupLDS, ~10 KB fp32), so a CU holds 16 envs (4 blocks of one wave: one wave per SIMD, the CU's
-// 160 KB) with no scratch spills and a compact instruction stream.  Same algorithm and operation order as physics.h (the per-lane kernel,
+// 160 KB; the kernel holds 512 VGPRs and spills 25 of them, 80 B of scratch per lane, tests/test_cpu_isa.py).
+// Same algorithm and operation order as physics.h (the per-lane kernel,
 // kept as the reference-shaped variant) except for the order of floating-point sums inside the
 // element-parallel ABA backward pass and the 16-lane DPP reductions of the PGS row products.
 //
@@ -116,6 +117,16 @@ constexpr TreeInfo tree_info() {
 }
 constexpr TreeInfo TREE = tree_info();
 static_assert(TREE.maxdepth < 8 && NB <= 21, "3-bit depth codes");
+// (S^T IA S + dt damping)^-1 of body b packed k x k (row major) from DINV_OFF[b]: sum k^2 = 35 words, not NB x 9
+struct DinvOff { int off[NB + 1]; };
+constexpr DinvOff dinv_off() {
+    DinvOff r{};
+    r.off[0] = 0;
+    for (int b = 0; b < NB; b++) r.off[b + 1] = r.off[b] + body_ndof[b] * body_ndof[b];
+    return r;
+}
+constexpr DinvOff DINV = dinv_off();
+constexpr int DINV_N = DINV.off[NB];
 __device__ inline int body_depth_l(int b) { return (int)((pack_bits<3>(TREE.depth) >> (3 * b)) & 7u); }
 __device__ inline int body_parent_l(int b) { return (int)((pack_bits<4>(TREE.parent0) >> (4 * b)) & 15u); }
 struct LinkInfo { int nlink[NB], link0[NB]; };
@@ -305,7 +316,10 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
     T tau[NDOF + 3];
     T nu[NV + 1];
     T R[NB][9], o[NB][3], Sc[NDOF][6];   // Sc: motion subspace column [u; o x u] of each hinge (world axes)
-    T U[NDOF][6], Dinv[NB][9], L0[21];
+    T U[NDOF][6], Dinv[DINV_N], L0[21];
+    // body velocities of the ABA's velocity nu* (before the constraint solve), written by pass 3: the friction
+    // rows' slip directions read them instead of re-summing the root path per row
+    T Vs[NB][6];
     union {
         struct {   // articulated-body pass (dead once the accelerations are known)
             T V[NB][6], c[NB][6], IA[NB][21], pA[NB][6], uu[NDOF + 1];   // V: pass-3 body accelerations
@@ -490,48 +504,10 @@ __device__ inline void chol6_solve_inv(const T* L, T* b) {
 }
 
 // ------------------------------------------------------------------------- test-impulse response
-// Same algorithm as physics.h::impulse_response, reading the ABA factorisation from LDS.
+// M^-1 J^T by the articulated-body solve of physics.h::impulse_response, reading the ABA factorisation from LDS.
+// the forward half: base acceleration from its articulated inertia, then root -> leaves
 template <typename T>
-__device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int bb, const T* fb, int jd, T jsign,
-                                  T* out) {
-    T pA[NB][6];
-#pragma unroll
-    for (int b = 0; b < NB; b++)
-#pragma unroll
-        for (int e = 0; e < 6; e++) pA[b][e] = (b == ba ? -fa[e] : T(0)) - (b == bb ? fb[e] : T(0));
-    T uq[NDOF];
-#pragma unroll
-    for (int b = NB - 1; b >= 1; b--) {
-        const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
-#pragma unroll
-        for (int j = 0; j < k; j++) {
-            const int d = d0 + j;
-            T Sc[6];
-            load_sc(S, d, Sc);
-            T s = (d == jd) ? jsign : T(0);
-#pragma unroll
-            for (int e = 0; e < 6; e++) s -= Sc[e] * pA[b][e];
-            uq[d] = s;
-        }
-        T w[3];
-#pragma unroll
-        for (int i = 0; i < k; i++) {
-            T t = 0;
-#pragma unroll
-            for (int j = 0; j < k; j++) t += S.Dinv[b][3 * i + j] * uq[d0 + j];
-            w[i] = t;
-        }
-#pragma unroll
-        for (int e = 0; e < 6; e++) {
-            T s = pA[b][e];
-#pragma unroll
-            for (int i = 0; i < k; i++) s += S.U[d0 + i][e] * w[i];
-            pA[p][e] += s;
-        }
-    }
-    T a[NB][6];
-#pragma unroll
-    for (int e = 0; e < 6; e++) a[0][e] = -pA[0][e];
+__device__ __attribute__((always_inline)) inline void g_response_fwd(const GroupLDS<T>& S, const T* uq, T (&a)[NB][6], T* out) {
     {
         T L[21];
 #pragma unroll
@@ -557,7 +533,7 @@ __device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int
         for (int i = 0; i < k; i++) {
             T s = 0;
 #pragma unroll
-            for (int j = 0; j < k; j++) s += S.Dinv[b][3 * i + j] * r[j];
+            for (int j = 0; j < k; j++) s += S.Dinv[DINV.off[b] + k * i + j] * r[j];
             out[6 + d0 + i] = s;
             const int d = d0 + i;
             T Sc[6];
@@ -566,6 +542,66 @@ __device__ inline void g_response(const GroupLDS<T>& S, int ba, const T* fa, int
             for (int e = 0; e < 6; e++) a[b][e] += Sc[e] * s;
         }
     }
+}
+
+
+struct TreeKids { bool leaf[NB]; int last_kid[NB]; };   // last_kid: the highest-index child (processed first)
+constexpr TreeKids tree_kids() {
+    TreeKids t{};
+    for (int b = 0; b < NB; b++) { t.leaf[b] = true; t.last_kid[b] = -1; }
+    for (int b = 1; b < NB; b++) {
+        t.leaf[body_parent[b]] = false;
+        if (b > t.last_kid[body_parent[b]]) t.last_kid[body_parent[b]] = b;
+    }
+    return t;
+}
+constexpr TreeKids KIDS = tree_kids();
+// The row's generalised impulse J^T drives the solve (physics.h::impulse_response injects the spatial forces on
+// its two bodies instead: the same linear map).  No per-body force selects (400 fewer VALU per row, +2.5 % measured,
+// profiles/r04_ab_rows.txt); the leaves receive no child contribution and each body's first child initialises its
+// parent's accumulator.  Rounding: a joint's impulse is J_d - S_d . pA (two rounded terms, where the force form
+// rounds S_d . (pA - f) once); measured over 512 lanes from identical states its fp32 error distribution is the
+// force form's (tools/diag_fp32_ab.py, profiles/r04_fp32ab.txt).
+template <typename T>
+__device__ inline void g_response(const GroupLDS<T>& S, const T* J, T* out) {
+    T pA[NB][6];   // the children's contributions to each body's articulated bias impulse
+    T uq[NDOF];
+#pragma unroll
+    for (int b = NB - 1; b >= 1; b--) {
+        const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
+#pragma unroll
+        for (int j = 0; j < k; j++) {
+            const int d = d0 + j;
+            T s = J[6 + d];
+            if (!KIDS.leaf[b]) {
+                T Sc[6];
+                load_sc(S, d, Sc);
+#pragma unroll
+                for (int e = 0; e < 6; e++) s -= Sc[e] * pA[b][e];
+            }
+            uq[d] = s;
+        }
+        T w[3];
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+            T t = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) t += S.Dinv[DINV.off[b] + k * i + j] * uq[d0 + j];
+            w[i] = t;
+        }
+#pragma unroll
+        for (int e = 0; e < 6; e++) {
+            T s = KIDS.leaf[b] ? T(0) : pA[b][e];
+#pragma unroll
+            for (int i = 0; i < k; i++) s += S.U[d0 + i][e] * w[i];
+            if (KIDS.last_kid[p] == b) pA[p][e] = s;
+            else pA[p][e] += s;
+        }
+    }
+    T a[NB][6];
+#pragma unroll
+    for (int e = 0; e < 6; e++) a[0][e] = J[e] - pA[0][e];
+    g_response_fwd(S, uq, a, out);
 }
 
 // J row for a spatial force f on body b (generic: runtime b)
@@ -607,49 +643,6 @@ __device__ inline void g_row_jacobian2(const GroupLDS<T>& S, int ba, const T* fa
 #pragma unroll
             for (int e = 0; e < 6; e++) { sa += fa[e] * Sc[e]; sb += fb[e] * Sc[e]; }
             J[6 + d] = (ona ? sa : T(0)) + (onb ? sb : T(0));
-        }
-    }
-}
-
-// spatial velocities of bodies ba and bb (bb < 0: Vb = 0) from nu, one pass over the dofs
-template <typename T>
-__device__ inline void g_body_vel2(const GroupLDS<T>& S, int ba, int bb, T* Va, T* Vb) {
-#pragma unroll
-    for (int e = 0; e < 6; e++) { Va[e] = S.nu[e]; Vb[e] = bb >= 0 ? S.nu[e] : T(0); }
-#pragma unroll
-    for (int x = 1; x < NB; x++) {
-        const bool ona = on_path(x, ba);
-        const bool onb = on_path(x, bb);
-#pragma unroll
-        for (int k = 0; k < body_ndof[x]; k++) {
-            const int d = body_dof0[x] + k;
-            T Sc[6];
-            load_sc(S, d, Sc);
-            const T qd = S.nu[6 + d];
-            const T qa = ona ? qd : T(0), qb = onb ? qd : T(0);
-#pragma unroll
-            for (int e = 0; e < 6; e++) { Va[e] += Sc[e] * qa; Vb[e] += Sc[e] * qb; }
-        }
-    }
-}
-
-// spatial velocity of body b from the generalised velocity nu (LDS)
-template <typename T>
-__device__ inline void g_body_vel(const GroupLDS<T>& S, int b, T* V) {
-#pragma unroll
-    for (int e = 0; e < 6; e++) V[e] = S.nu[e];
-#pragma unroll
-    for (int x = 1; x < NB; x++) {
-        const bool on = on_path(x, b);
-#pragma unroll
-        for (int k = 0; k < body_ndof[x]; k++) {
-            const int d = body_dof0[x] + k;
-            T Sc[6];
-            load_sc(S, d, Sc);
-            const T qd = S.nu[6 + d];
-            if (on)
-#pragma unroll
-                for (int e = 0; e < 6; e++) V[e] += Sc[e] * qd;
         }
     }
 }
@@ -786,7 +779,8 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 dir[0] = n[0]; dir[1] = n[1]; dir[2] = n[2];
             } else {
                 T Va[6], Vb[6], va[3], vb[3], vr[3];
-                g_body_vel2(S, ba, bb, Va, Vb);
+#pragma unroll
+                for (int e = 0; e < 6; e++) { Va[e] = S.Vs[ba][e]; Vb[e] = bb >= 0 ? S.Vs[bb >= 0 ? bb : 0][e] : T(0); }
                 cross3(Va, pa, va);
                 cross3(Vb, pb, vb);
 #pragma unroll
@@ -820,7 +814,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
 #pragma unroll
         for (int k = 0; k < NDOF; k++)
             if (k == jd) J[6 + k] = jsign;
-        g_response(S, ba, fa, bb, fb, jd, jsign, Mi);
+        g_response(S, J, Mi);
         T jm = 0;
 #pragma unroll
         for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];   // limit rows: sg * Mi[6 + d] (sg^2 = 1)
@@ -984,8 +978,12 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
             A.uu[d0 + j] = uj[j];
         }
     }
+    const int doff = lvl_sel<LV>(g, [](int x) { return DINV.off[x]; });
 #pragma unroll
-    for (int q = 0; q < 9; q++) S.Dinv[b][q] = Di[q];
+    for (int i = 0; i < KM; i++)
+#pragma unroll
+        for (int j = 0; j < KM; j++)
+            if (i < k && j < k) S.Dinv[doff + k * i + j] = Di[3 * i + j];
 }
 
 // ------------------------------------------------------------------------- ABA pass 3, one tree level
@@ -1004,11 +1002,12 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
     const int p = sel([](int x) { return body_parent[x]; });
     const int k = sel([](int x) { return body_ndof[x]; });
     const int d0 = sel([](int x) { return body_dof0[x]; });
+    const int doff = sel([](int x) { return DINV.off[x]; });
     constexpr int KM = [] { int m = 0; for (int i = 0; i < 4; i++) m = body_ndof[FWD_BODY[LV][i]] > m ? body_ndof[FWD_BODY[LV][i]] : m; return m; }();
     const T vmax = (T)P.max_coord_vel;
-    T ap[6], r[3], ab[6];
+    T ap[6], r[3], ab[6], vs[6];
 #pragma unroll
-    for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + A.c[b][e]; ab[e] = ap[e]; }
+    for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + A.c[b][e]; ab[e] = ap[e]; vs[e] = S.Vs[p][e]; }
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         const int d = j < k ? d0 + j : d0;
@@ -1021,7 +1020,7 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
     for (int i = 0; i < KM; i++) {
         T t = 0;
 #pragma unroll
-        for (int j = 0; j < KM; j++) t += S.Dinv[b][3 * i + j] * r[j];   // padded block: identity, r = 0
+        for (int j = 0; j < KM; j++) t += (i < k && j < k ? S.Dinv[doff + k * i + j] : T(0)) * r[j];   // padded: r = 0
         const int d = i < k ? d0 + i : d0;
         T Sc[6];
         load_sc(S, d, Sc);
@@ -1030,9 +1029,14 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
         for (int e = 0; e < 6; e++) ab[e] += Sc[e] * qdd;
         const T nn = clampT(S.nu[6 + d] + dt * qdd, -vmax, vmax);
         if (i < k) S.nu[6 + d] = nn;
+        // the body's velocity of nu*: its parent's plus its own dofs, in root-path order (the sums a per-row path
+        // walk would form, in the same order)
+        const T qn = i < k ? nn : T(0);
+#pragma unroll
+        for (int e = 0; e < 6; e++) vs[e] += Sc[e] * qn;
     }
 #pragma unroll
-    for (int e = 0; e < 6; e++) A.V[b][e] = ab[e];
+    for (int e = 0; e < 6; e++) { A.V[b][e] = ab[e]; S.Vs[b][e] = vs[e]; }
 }
 
 // ------------------------------------------------------------------------- one cooperative substep
@@ -1238,9 +1242,19 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         chol6_solve_inv(L, a0);
 #pragma unroll
         for (int e = 0; e < 6; e++) nub[e] = S.nu[e];
+        T nus[6];   // the base's nu*: the torso's velocity for the forward levels' body velocities
+        {
+            T wxv[3];
+            cross3(nub, nub + 3, wxv);
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                nus[i] = clampT(nub[i] + dt * a0[i], -vmax, vmax);
+                nus[3 + i] = clampT(nub[3 + i] + dt * (a0[3 + i] + wxv[i]), -vmax, vmax);
+            }
+        }
         if (l == 0) {
 #pragma unroll
-            for (int e = 0; e < 6; e++) A.V[0][e] = a0[e];
+            for (int e = 0; e < 6; e++) { A.V[0][e] = a0[e]; S.Vs[0][e] = nus[e]; }
         }
         wave_sync();
         SUBPHASE(15);
@@ -1252,15 +1266,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         wave_sync();
         group_fwd_level<T, 3>(P, S, l >> 2, dt);
         if (l == 0) {
-            T wxv[3];
-            cross3(nub, nub + 3, wxv);
 #pragma unroll
             for (int q = 0; q < 21; q++) S.L0[q] = L[q];
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
-                S.nu[i] = clampT(nub[i] + dt * a0[i], -vmax, vmax);
-                S.nu[3 + i] = clampT(nub[3 + i] + dt * (a0[3 + i] + wxv[i]), -vmax, vmax);
-            }
+            for (int e = 0; e < 6; e++) S.nu[e] = nus[e];
         }
     }
     __syncthreads();
