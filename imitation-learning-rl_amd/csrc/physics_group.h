@@ -129,6 +129,37 @@ constexpr DinvOff DINV = dinv_off();
 constexpr int DINV_N = DINV.off[NB];
 __device__ inline int body_depth_l(int b) { return (int)((pack_bits<3>(TREE.depth) >> (3 * b)) & 7u); }
 __device__ inline int body_parent_l(int b) { return (int)((pack_bits<4>(TREE.parent0) >> (4 * b)) & 15u); }
+// the hinge dofs on body b's root path (its ancestors' and its own, root to leaf = ascending dof order) as at most two
+// contiguous runs: [0, e1) and [s2, s2 + len - e1)
+struct PathRuns { int e1[NB], s2[NB], len[NB]; bool ok; };
+constexpr PathRuns path_runs() {
+    PathRuns r{};
+    r.ok = true;
+    for (int b = 0; b < NB; b++) {
+        bool on[NDOF] = {};
+        int len = 0;
+        for (int y = b; y > 0; y = body_parent[y])
+            for (int k = 0; k < body_ndof[y]; k++) { on[body_dof0[y] + k] = true; len++; }
+        int e1 = 0;
+        while (e1 < NDOF && on[e1]) e1++;
+        int s2 = e1;
+        while (s2 < NDOF && !on[s2]) s2++;
+        if (len == e1) s2 = 0;
+        for (int d = 0; d < NDOF; d++)
+            if (on[d] != (d < e1 || (d >= s2 && d < s2 + len - e1))) r.ok = false;
+        r.e1[b] = e1; r.s2[b] = s2; r.len[b] = len;
+    }
+    return r;
+}
+constexpr PathRuns PATHS = path_runs();
+static_assert(PATHS.ok, "every root path is at most two contiguous dof runs, the first from dof 0");
+constexpr int PATH_LEN_MAX = [] { int m = 0; for (int b = 0; b < NB; b++) m = PATHS.len[b] > m ? PATHS.len[b] : m; return m; }();
+static_assert(PATH_LEN_MAX < 8 && NDOF < 32, "3-bit path lengths, 5-bit dof indices");
+// the longest parent path (a body's parent velocity sums it)
+constexpr int PPATH_MAX = [] { int m = 0; for (int b = 1; b < NB; b++) m = PATHS.len[body_parent[b]] > m ? PATHS.len[body_parent[b]] : m; return m; }();
+__device__ inline int path_e1_l(int b) { return (int)((pack_bits<3>(PATHS.e1) >> (3 * b)) & 7u); }
+__device__ inline int path_s2_l(int b) { return (int)((pack_bits<5>(PATHS.s2) >> (5 * b)) & 31u); }
+__device__ inline int path_len_l(int b) { return (int)((pack_bits<3>(PATHS.len) >> (3 * b)) & 7u); }
 struct LinkInfo { int nlink[NB], link0[NB]; };
 constexpr LinkInfo link_info() {
     LinkInfo r{};
@@ -322,7 +353,10 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
     T Vs[NB][6];
     union {
         struct {   // articulated-body pass (dead once the accelerations are known)
-            T V[NB][6], c[NB][6], IA[NB][21], pA[NB][6], uu[NDOF + 1];   // V: pass-3 body accelerations
+            // IA rows padded to 24 words: 16-byte aligned, so a row moves in six 16-byte LDS accesses
+            T V[NB][6], c[NB][6];
+            alignas(16) T IA[NB][24];
+            T pA[NB][6], uu[NDOF + 1];   // V: pass-3 body accelerations
         } aba;
         struct {   // contacts + constraint rows
             T gp[NGEOM][2][3];
@@ -425,6 +459,8 @@ static __shared__ unsigned long long s_tlast;   // shared: markers also sit insi
 
 #if defined(HUM_WAVE_LOG) && defined(HUM_SUBPHASE)   // finer split of a phase's time (tools/wave_log.py)
 #define SUBPHASE(k) PHASE(k)
+#elif defined(HUM_PHASE_MARK) && defined(HUM_SUBPHASE)   // static ISA attribution of the sub-phases
+#define SUBPHASE(k) asm volatile("; @sub " #k ::: "memory")
 #else
 #define SUBPHASE(k) do { } while (0)
 #endif
@@ -1093,43 +1129,26 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     __syncthreads();
     PHASE(1);
-    // ---- body velocities root -> leaves, one tree depth per step (lane b = body b at that depth):
-    //      Vt[b] = Vt[parent] + sum over b's dofs of Sc * qd, the same additions in the same order as summing the
-    //      whole root path on every lane (4 short steps instead of 17 dofs of masked FMAs per lane).  Scratch:
-    //      the ABA's V slots, which pass 3 overwrites.
-    {
-        T* Vt = &S.x.aba.V[0][0];
-        if (l < 6) Vt[l] = S.nu[l];
-#pragma unroll
-        for (int lv = 1; lv <= TREE.maxdepth; lv++) {
-            wave_sync();
-            if (l < NB && body_depth_l(l) == lv) {
-                const int b = l, p = body_parent_l(b), k = body_ndof_l(b), d0 = body_dof0_l(b);
-                T v[6];
-#pragma unroll
-                for (int e = 0; e < 6; e++) v[e] = Vt[6 * p + e];
-                for (int j = 0; j < k; j++) {
-                    const int d = d0 + j;
-                    T Sc[6];
-                    load_sc(S, d, Sc);
-                    const T qd = S.nu[6 + d];
-#pragma unroll
-                    for (int e = 0; e < 6; e++) v[e] += Sc[e] * qd;
-                }
-#pragma unroll
-                for (int e = 0; e < 6; e++) Vt[6 * b + e] = v[e];
-            }
-        }
-        wave_sync();
-    }
     // ---- ABA pass 1: lane b = body b
     if (l < NB) {
         const int b = l;
         T V[6];
-        {   // parent velocity (the torso: the base velocity itself)
-            const int p = body_parent_l(b);
+        {   // parent velocity: the base velocity plus the parent's root-path dofs in path order (the sums a tree-depth
+            // sweep forms, without its 4 synchronised steps; the torso: the base velocity itself)
+            const int p = body_parent_l(b), e1 = path_e1_l(p), s2 = path_s2_l(p), n = path_len_l(p);
 #pragma unroll
-            for (int e = 0; e < 6; e++) V[e] = S.x.aba.V[p][e];
+            for (int e = 0; e < 6; e++) V[e] = S.nu[e];
+#pragma unroll
+            for (int j = 0; j < PPATH_MAX; j++) {
+                if (j < n) {
+                    const int d = j < e1 ? j : s2 + (j - e1);
+                    T Sc[6];
+                    load_sc(S, d, Sc);
+                    const T qd = S.nu[6 + d];
+#pragma unroll
+                    for (int e = 0; e < 6; e++) V[e] += Sc[e] * qd;
+                }
+            }
         }
         SUBPHASE(13);
         T cb[6] = {0, 0, 0, 0, 0, 0};
@@ -1581,6 +1600,15 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 n0 = fma(X.m0, dl, n0);
                 n1 += X.m1 * dl;
                 dlp = dl;
+                // the row read this stage must have landed by its end: keeps the scheduler from sinking its loads
+                // next to their first use two stages on, where the LDS latency was exposed (+1.1 %,
+                // profiles/r04_ab_rows.txt)
+#ifdef HUM_PGS_PINALL   // experiment: every field of the row, and the bounding lambda
+                asm volatile("" ::"v"(W.j0), "v"(W.m0), "v"(W.j1), "v"(W.m1), "v"(W.b), "v"(W.meff), "v"(W.hi), "v"(W.lam),
+                             "v"(W.mu), "v"(W.q), "v"(W.next3), "v"(W.next3_ln), "v"(lnW));
+#else
+                asm volatile("" ::"v"(W.j0), "v"(W.m0), "v"(W.j1), "v"(W.m1), "v"(W.b), "v"(W.meff));
+#endif
             };
             auto round = [&](auto masked, int k) {
                 stage(masked, k, A, B, D, oA, oD, pA, pB, lnA, lnD);
