@@ -885,8 +885,28 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 T* Rr = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(epos + qr));
                 const T* Rp = reinterpret_cast<const T*>(reinterpret_cast<const char*>(shb) + pool_off<T>(epos + qp));
                 T c = 0;
+                if constexpr (sizeof(T) == 4) {
+                    // 16-byte reads of (J, M^-1 J^T) pair couples, all issued before the sum needs them (the pairwise
+                    // scalar reads were issued two at a time, each pair waited for)
+                    static_assert(RO_Z == 2 * NV && NV % 2 == 1, "the last quad holds pair NV - 1 and the zero pair");
+                    using f4v = float __attribute__((ext_vector_type(4)));
+                    f4v a4[(NV + 1) / 2], b4[(NV + 1) / 2];
 #pragma unroll
-                for (int q = 0; q < NV; q++) c += Rr[2 * q] * Rp[2 * q + 1];
+                    for (int h = 0; h < (NV + 1) / 2; h++) {
+                        a4[h] = reinterpret_cast<const f4v*>(Rr)[h];
+                        b4[h] = reinterpret_cast<const f4v*>(Rp)[h];
+                    }
+#pragma unroll
+                    for (int h = 0; h < (NV + 1) / 2; h++) asm volatile("" ::"v"(a4[h]), "v"(b4[h]));   // whole quads, in flight together
+#pragma unroll
+                    for (int h = 0; h < (NV + 1) / 2; h++) {
+                        c += a4[h].x * b4[h].y;
+                        if (2 * h + 1 < NV) c += a4[h].z * b4[h].w;
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < NV; q++) c += Rr[2 * q] * Rp[2 * q + 1];
+                }
                 Rr[RO_S1 + 1] = c * Rr[RO_S0 + 3];   // q_r = meff_r c_r: the PGS scalar chain multiplies it by dl
             }
         }
@@ -917,19 +937,49 @@ __device__ __attribute__((always_inline)) inline T lvl_damp(int g, int j) {
     return g == 0 ? v[0] : (g == 1 ? v[1] : (g == 2 ? v[2] : v[3]));
 }
 
+// The inputs of a level's body that pass 1 (or the FK) wrote: loaded one level early, while the previous level
+// computes, so the LDS latency of only the children's contributions stays on the level-to-level chain.
+template <typename T>
+struct AbaIn { T IA[21], pA[6], c[6], Sc[3][6], tau[3], qd[3]; };
+template <int LV>
+constexpr int aba_km() {   // the level's largest dof count (1, 3, 1, 2): smaller bodies of the level are padded to it
+    int m = 0;
+    for (int i = 0; i < 4; i++) m = body_ndof[LVL_BODY[LV][i]] > m ? body_ndof[LVL_BODY[LV][i]] : m;
+    return m;
+}
 template <typename T, int LV>
-__device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt) {
+__device__ __attribute__((always_inline)) void aba_load(const GroupLDS<T>& S, const int g, AbaIn<T>& in) {
+    const auto& A = S.x.aba;
+    constexpr int KM = aba_km<LV>();
+    const int b = lvl_sel<LV>(g, [](int x) { return x; });
+    const int k = lvl_sel<LV>(g, [](int x) { return body_ndof[x]; });
+    const int d0 = lvl_sel<LV>(g, [](int x) { return body_dof0[x]; });
+#pragma unroll
+    for (int q = 0; q < 21; q++) in.IA[q] = A.IA[b][q];
+#pragma unroll
+    for (int e = 0; e < 6; e++) { in.pA[e] = A.pA[b][e]; in.c[e] = A.c[b][e]; }
+#pragma unroll
+    for (int j = 0; j < KM; j++) {
+        const int d = j < k ? d0 + j : d0;
+        load_sc(S, d, in.Sc[j]);
+        in.tau[j] = S.tau[d];
+        in.qd[j] = S.nu[6 + d];
+    }
+}
+
+template <typename T, int LV>
+__device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt,
+                                                               const AbaIn<T>& in) {
     auto& A = S.x.aba;
-    // the level's largest dof count (1, 3, 1, 2): smaller bodies of the level are padded to it
-    constexpr int KM = [] { int m = 0; for (int i = 0; i < 4; i++) m = body_ndof[LVL_BODY[LV][i]] > m ? body_ndof[LVL_BODY[LV][i]] : m; return m; }();
+    constexpr int KM = aba_km<LV>();
     const int b = lvl_sel<LV>(g, [](int x) { return x; });
     const int k = lvl_sel<LV>(g, [](int x) { return body_ndof[x]; });
     const int d0 = lvl_sel<LV>(g, [](int x) { return body_dof0[x]; });
     T IA[21], pAb[6], cb[6], Sc[3][6], U[3][6], D[9], Di[9], uj[3], W[3][6];
 #pragma unroll
-    for (int q = 0; q < 21; q++) IA[q] = A.IA[b][q];
+    for (int q = 0; q < 21; q++) IA[q] = in.IA[q];
 #pragma unroll
-    for (int e = 0; e < 6; e++) { pAb[e] = A.pA[b][e]; cb[e] = A.c[b][e]; }
+    for (int e = 0; e < 6; e++) { pAb[e] = in.pA[e]; cb[e] = in.c[e]; }
     auto add_kid = [&](int kid) {
 #pragma unroll
         for (int q = 0; q < 21; q++) IA[q] += A.IA[kid][q];
@@ -944,16 +994,14 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         const bool on = j < k;
-        const int d = on ? d0 + j : d0;
-        load_sc(S, d, Sc[j]);
 #pragma unroll
-        for (int e = 0; e < 6; e++) Sc[j][e] = on ? Sc[j][e] : T(0);
+        for (int e = 0; e < 6; e++) Sc[j][e] = on ? in.Sc[j][e] : T(0);
         symmv(IA, Sc[j], U[j]);
         T sp = 0;
 #pragma unroll
         for (int e = 0; e < 6; e++) sp += Sc[j][e] * pAb[e];
-        T t = S.tau[d] - sp;
-        if (P.joint_damping) t -= lvl_damp<LV, T>(g, j) * S.nu[6 + d];
+        T t = in.tau[j] - sp;
+        if (P.joint_damping) t -= lvl_damp<LV, T>(g, j) * in.qd[j];
         uj[j] = on ? t : T(0);
     }
 #pragma unroll
@@ -1027,49 +1075,79 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 // travel through the dead pass-1 velocity slots A.V.  Each group integrates its own dofs into nu*
 // (groups sharing a body compute and write identical values).
 constexpr int FWD_BODY[4][4] = {{1, 7, 9, 9}, {2, 8, 10, 10}, {3, 5, 3, 5}, {4, 6, 4, 6}};
+template <int LV>
+constexpr int fwd_km() {
+    int m = 0;
+    for (int i = 0; i < 4; i++) m = body_ndof[FWD_BODY[LV][i]] > m ? body_ndof[FWD_BODY[LV][i]] : m;
+    return m;
+}
+template <int LV, typename F>
+__device__ __attribute__((always_inline)) inline int fwd_sel(int g, F f) {   // per-group compile-time value
+    const int v0 = f(FWD_BODY[LV][0]), v1 = f(FWD_BODY[LV][1]), v2 = f(FWD_BODY[LV][2]), v3 = f(FWD_BODY[LV][3]);
+    return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+}
+// a level's inputs from pass 2 and the FK (everything but the parent's acceleration and velocity), loaded one level
+// early like pass 2's (AbaIn)
+template <typename T>
+struct FwdIn { T c[6], U[3][6], uu[3], Dinv[9], Sc[3][6], nu[3]; };
 template <typename T, int LV>
-__device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt) {
-    auto& A = S.x.aba;
-    auto sel = [&](auto f) {
-        const int v0 = f(FWD_BODY[LV][0]), v1 = f(FWD_BODY[LV][1]), v2 = f(FWD_BODY[LV][2]), v3 = f(FWD_BODY[LV][3]);
-        return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
-    };
-    const int b = sel([](int x) { return x; });
-    const int p = sel([](int x) { return body_parent[x]; });
-    const int k = sel([](int x) { return body_ndof[x]; });
-    const int d0 = sel([](int x) { return body_dof0[x]; });
-    const int doff = sel([](int x) { return DINV.off[x]; });
-    constexpr int KM = [] { int m = 0; for (int i = 0; i < 4; i++) m = body_ndof[FWD_BODY[LV][i]] > m ? body_ndof[FWD_BODY[LV][i]] : m; return m; }();
-    const T vmax = (T)P.max_coord_vel;
-    T ap[6], r[3], ab[6], vs[6];
+__device__ __attribute__((always_inline)) void fwd_load(const GroupLDS<T>& S, const int g, FwdIn<T>& in) {
+    const auto& A = S.x.aba;
+    constexpr int KM = fwd_km<LV>();
+    const int b = fwd_sel<LV>(g, [](int x) { return x; });
+    const int k = fwd_sel<LV>(g, [](int x) { return body_ndof[x]; });
+    const int d0 = fwd_sel<LV>(g, [](int x) { return body_dof0[x]; });
+    const int doff = fwd_sel<LV>(g, [](int x) { return DINV.off[x]; });
 #pragma unroll
-    for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + A.c[b][e]; ab[e] = ap[e]; vs[e] = S.Vs[p][e]; }
+    for (int e = 0; e < 6; e++) in.c[e] = A.c[b][e];
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         const int d = j < k ? d0 + j : d0;
-        T t = A.uu[d];
 #pragma unroll
-        for (int e = 0; e < 6; e++) t -= S.U[d][e] * ap[e];
+        for (int e = 0; e < 6; e++) in.U[j][e] = S.U[d][e];
+        in.uu[j] = A.uu[d];
+        load_sc(S, d, in.Sc[j]);
+        in.nu[j] = S.nu[6 + d];
+#pragma unroll
+        for (int i = 0; i < KM; i++) in.Dinv[3 * i + j] = i < k && j < k ? S.Dinv[doff + k * i + j] : T(0);   // padded: 0
+    }
+}
+template <typename T, int LV>
+__device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt,
+                                                               const FwdIn<T>& in) {
+    auto& A = S.x.aba;
+    const int b = fwd_sel<LV>(g, [](int x) { return x; });
+    const int p = fwd_sel<LV>(g, [](int x) { return body_parent[x]; });
+    const int k = fwd_sel<LV>(g, [](int x) { return body_ndof[x]; });
+    const int d0 = fwd_sel<LV>(g, [](int x) { return body_dof0[x]; });
+    constexpr int KM = fwd_km<LV>();
+    const T vmax = (T)P.max_coord_vel;
+    T ap[6], r[3], ab[6], vs[6];
+#pragma unroll
+    for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + in.c[e]; ab[e] = ap[e]; vs[e] = S.Vs[p][e]; }
+#pragma unroll
+    for (int j = 0; j < KM; j++) {
+        T t = in.uu[j];
+#pragma unroll
+        for (int e = 0; e < 6; e++) t -= in.U[j][e] * ap[e];
         r[j] = j < k ? t : T(0);
     }
 #pragma unroll
     for (int i = 0; i < KM; i++) {
         T t = 0;
 #pragma unroll
-        for (int j = 0; j < KM; j++) t += (i < k && j < k ? S.Dinv[doff + k * i + j] : T(0)) * r[j];   // padded: r = 0
+        for (int j = 0; j < KM; j++) t += in.Dinv[3 * i + j] * r[j];   // padded block: 0, r = 0
         const int d = i < k ? d0 + i : d0;
-        T Sc[6];
-        load_sc(S, d, Sc);
         const T qdd = i < k ? t : T(0);
 #pragma unroll
-        for (int e = 0; e < 6; e++) ab[e] += Sc[e] * qdd;
-        const T nn = clampT(S.nu[6 + d] + dt * qdd, -vmax, vmax);
+        for (int e = 0; e < 6; e++) ab[e] += in.Sc[i][e] * qdd;
+        const T nn = clampT(in.nu[i] + dt * qdd, -vmax, vmax);
         if (i < k) S.nu[6 + d] = nn;
         // the body's velocity of nu*: its parent's plus its own dofs, in root-path order (the sums a per-row path
         // walk would form, in the same order)
         const T qn = i < k ? nn : T(0);
 #pragma unroll
-        for (int e = 0; e < 6; e++) vs[e] += Sc[e] * qn;
+        for (int e = 0; e < 6; e++) vs[e] += in.Sc[i][e] * qn;
     }
 #pragma unroll
     for (int e = 0; e < 6; e++) { A.V[b][e] = ab[e]; S.Vs[b][e] = vs[e]; }
@@ -1238,13 +1316,20 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     //      contributions, and overwrites its IA/pA slots with its contribution to the parent (no longer
     //      needed itself).  The base step below sums the torso with lwaist and both upper arms.
     auto& A = S.x.aba;
-    group_aba_level<T, 0>(P, S, l >> 2, dt);
-    wave_sync();
-    group_aba_level<T, 1>(P, S, l >> 2, dt);
-    wave_sync();
-    group_aba_level<T, 2>(P, S, l >> 2, dt);
-    wave_sync();
-    group_aba_level<T, 3>(P, S, l >> 2, dt);
+    {
+        AbaIn<T> in0, in1;
+        aba_load<T, 0>(S, l >> 2, in0);
+        aba_load<T, 1>(S, l >> 2, in1);
+        group_aba_level<T, 0>(P, S, l >> 2, dt, in0);
+        wave_sync();
+        aba_load<T, 2>(S, l >> 2, in0);
+        group_aba_level<T, 1>(P, S, l >> 2, dt, in1);
+        wave_sync();
+        aba_load<T, 3>(S, l >> 2, in1);
+        group_aba_level<T, 2>(P, S, l >> 2, dt, in0);
+        wave_sync();
+        group_aba_level<T, 3>(P, S, l >> 2, dt, in1);
+    }
     __syncthreads();
     PHASE(3);
     // ---- base + pass 3 (redundant on every lane); lane 0 publishes L0 and nu* = clamp(nu + dt acc)
@@ -1252,6 +1337,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         // base (redundant on every lane), then the forward pass by tree level (root -> leaves, one body per
         // 4-lane group, see group_fwd_level); lane 0 integrates the base and publishes L0 (inverse-diagonal form)
         const T vmax = (T)P.max_coord_vel;
+        FwdIn<T> fin0, fin1;
+        fwd_load<T, 0>(S, l >> 2, fin0);   // read while the base solve runs
         T L[21], a0[6], IA0[21], nub[6];
 #pragma unroll
         for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q] + A.IA[1][q] + A.IA[7][q] + A.IA[9][q];   // torso + kids
@@ -1277,13 +1364,16 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         }
         wave_sync();
         SUBPHASE(15);
-        group_fwd_level<T, 0>(P, S, l >> 2, dt);
+        fwd_load<T, 1>(S, l >> 2, fin1);
+        group_fwd_level<T, 0>(P, S, l >> 2, dt, fin0);
         wave_sync();
-        group_fwd_level<T, 1>(P, S, l >> 2, dt);
+        fwd_load<T, 2>(S, l >> 2, fin0);
+        group_fwd_level<T, 1>(P, S, l >> 2, dt, fin1);
         wave_sync();
-        group_fwd_level<T, 2>(P, S, l >> 2, dt);
+        fwd_load<T, 3>(S, l >> 2, fin1);
+        group_fwd_level<T, 2>(P, S, l >> 2, dt, fin0);
         wave_sync();
-        group_fwd_level<T, 3>(P, S, l >> 2, dt);
+        group_fwd_level<T, 3>(P, S, l >> 2, dt, fin1);
         if (l == 0) {
 #pragma unroll
             for (int q = 0; q < 21; q++) S.L0[q] = L[q];
@@ -1603,12 +1693,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 // the row read this stage must have landed by its end: keeps the scheduler from sinking its loads
                 // next to their first use two stages on, where the LDS latency was exposed (+1.1 %,
                 // profiles/r04_ab_rows.txt)
-#ifdef HUM_PGS_PINALL   // experiment: every field of the row, and the bounding lambda
-                asm volatile("" ::"v"(W.j0), "v"(W.m0), "v"(W.j1), "v"(W.m1), "v"(W.b), "v"(W.meff), "v"(W.hi), "v"(W.lam),
-                             "v"(W.mu), "v"(W.q), "v"(W.next3), "v"(W.next3_ln), "v"(lnW));
-#else
+                // (pinning every field of the row and its bounding lambda as well measured the same)
                 asm volatile("" ::"v"(W.j0), "v"(W.m0), "v"(W.j1), "v"(W.m1), "v"(W.b), "v"(W.meff));
-#endif
             };
             auto round = [&](auto masked, int k) {
                 stage(masked, k, A, B, D, oA, oD, pA, pB, lnA, lnD);
