@@ -207,6 +207,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     if G and (G % k or steps % k):
         raise SystemExit("--gather-every: it and --steps must be multiples of --k")
     ring = [None] * (G // k if G else 1)   # output buffers of the launches since the last gather
+    rem_out = {}   # output buffers of the shorter remainder launches, by size
     if a.hier:
         from ilrl_amd.hier_env import HierVecEnv
         env = HierVecEnv(n, seed=0, device=dev.index, lane_offset=rank * n, precision=precision, block_size=a.block,
@@ -215,7 +216,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         def step(s, kk=k):
             j = s % len(ring)
             if kk < k:   # the remainder launch
-                return env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True)
+                return env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True, out=rem_out.get(kk))
             ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:   # config 5 closed loop: both levels' policies on the device (hum_hier_rollout)
             from ilrl_amd.policy import DevicePolicy, hier_rollout
@@ -238,7 +239,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         def step(s, kk=k):
             j = s % len(ring)
             if kk < k:   # the remainder launch
-                return env.step_k(pool[s % 16][:kk], autoreset=True)
+                return env.step_k(pool[s % 16][:kk], autoreset=True, out=rem_out.get(kk))
             ring[j] = env.step_k(pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:
             from ilrl_amd.policy import DevicePolicy
@@ -256,6 +257,16 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     for w in range(wlaunches):
         step(w, wsizes[w])
     gather_s, gathered = 0.0, []
+    if not a.policy:
+        # every output buffer the timed launches write exists before the clock starts (a warmup shorter than k, e.g.
+        # the driver's --steps 20 --warmup 5, never ran a launch of the timed shape: its allocation and zero fill
+        # were timed)
+        for j in range(len(ring)):
+            if ring[j] is None:
+                ring[j] = env.step_k_out(k)
+        for kk in set(sizes):
+            if kk < k:
+                rem_out[kk] = env.step_k_out(kk)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

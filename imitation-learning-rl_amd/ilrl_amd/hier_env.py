@@ -88,16 +88,20 @@ class HierVecEnv(HumanoidVecEnv):
             raise ValueError("actions must be [k, %d, 2] and [k, %d, 17]" % (self.n, self.n))
         ag = None if agent is None else t.as_tensor(agent, dtype=t.uint8, device=self.device).expand(k, self.n).contiguous()
         if out is None or out[0].shape[0] != k:
-            f32 = t.float32
-            z = lambda *s, d=f32: t.zeros(*s, dtype=d, device=self.device)
-            out = (z(k, self.n, d=t.uint8), z(k, self.n, N.HUM_NOBS_HIGH), z(k, self.n, N.HUM_NOBS), z(k, self.n),
-                   z(k, self.n), z(k, self.n, d=t.uint8), z(k, self.n, d=t.int32), z(k, self.n, N.HUM_NOBS_HIGH))
+            out = self.step_k_out(k)
         agents, oh, ol, rh, rl, done, frame, ohr = out
         flags = (N.HUM_STEP_AUTORESET if autoreset else 0) | (N.HUM_STEP_SKIP_PHYSICS if skip_physics else 0)
         N.check(N.lib().hum_hier_step_k(self.h, _ptr(ah), _ptr(al), _ptr(ag), _ptr(agents), _ptr(oh), _ptr(ol),
                                         _ptr(rh), _ptr(rl), _ptr(done), _ptr(frame), flags, _ptr(ohr), k,
                                         self._stream()), "hum_hier_step_k")
         return out
+
+    def step_k_out(self, k):
+        """A zeroed output tuple for step_k(..., out=) of k transitions (allocate it ahead of a timed loop)."""
+        t, f32 = self.torch, self.torch.float32
+        z = lambda *s, d=f32: t.zeros(*s, dtype=d, device=self.device)
+        return (z(k, self.n, d=t.uint8), z(k, self.n, N.HUM_NOBS_HIGH), z(k, self.n, N.HUM_NOBS), z(k, self.n),
+                z(k, self.n), z(k, self.n, d=t.uint8), z(k, self.n, d=t.int32), z(k, self.n, N.HUM_NOBS_HIGH))
 
 
 class _HierBookView(_BookView):

@@ -148,17 +148,21 @@ class HumanoidVecEnv:
             raise ValueError("actions must be [k, %d, %d], got %s" % (self.n, N.HUM_NACT, tuple(a.shape)))
         k = a.shape[0]
         if out is None or out[0].shape[0] != k:
-            f32 = t.float32
-            out = (t.zeros(k, self.n, N.HUM_NOBS, dtype=f32, device=self.device),
-                   t.zeros(k, self.n, dtype=f32, device=self.device),
-                   t.zeros(k, self.n, dtype=t.uint8, device=self.device),
-                   t.zeros(k, self.n, dtype=t.int32, device=self.device),
-                   t.zeros(k, self.n, N.HUM_NOBS, dtype=f32, device=self.device))
+            out = self.step_k_out(k)
         obs, rew, done, frame, obs_reset = out
         flags = (N.HUM_STEP_AUTORESET if autoreset else 0) | (N.HUM_STEP_SKIP_PHYSICS if skip_physics else 0)
         N.check(N.lib().hum_step_k(self.h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(done), _ptr(frame), flags,
                                    _ptr(obs_reset), k, self._stream()), "hum_step_k")
         return out
+
+    def step_k_out(self, k):
+        """A zeroed output tuple for step_k(..., out=) of k steps (allocate it ahead of a timed loop)."""
+        t, f32 = self.torch, self.torch.float32
+        return (t.zeros(k, self.n, N.HUM_NOBS, dtype=f32, device=self.device),
+                t.zeros(k, self.n, dtype=f32, device=self.device),
+                t.zeros(k, self.n, dtype=t.uint8, device=self.device),
+                t.zeros(k, self.n, dtype=t.int32, device=self.device),
+                t.zeros(k, self.n, N.HUM_NOBS, dtype=f32, device=self.device))
 
     def get_aux(self):
         N.check(N.lib().hum_get_aux(self.h, _ptr(self.aux), self._stream()), "hum_get_aux")
