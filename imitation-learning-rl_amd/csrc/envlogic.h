@@ -129,9 +129,22 @@ struct PostPhys {   // physics-derived quantities calc_state reads (pybullet get
 };
 
 // WalkerBase.calc_state (pybullet_envs/robot_locomotors.py) -> 42 float32 + side effects
+// calc_state's joint block for one dof: obs 8 + 2d (relative position) and 9 + 2d (speed) before the observation clamp,
+// and whether the joint counts as at its limit (the cooperative kernel computes the 17 dofs on 17 lanes)
+template <typename T>
+__device__ inline bool joint_obs(const T* st, int d, float& rp, float& rv) {
+    const double q = (double)st[13 + d], qd = (double)st[30 + d];
+    const double lo = dof_lo[d], hi = dof_hi[d];
+    const double mid = 0.5 * (lo + hi);
+    rp = (float)(2 * (q - mid) / (hi - lo));
+    rv = (float)(qd * 0.1);
+    return fabsf(rp) > 0.99f;
+}
+
+// joints = false: the joint block (obs 8..41, joint_speeds, joints_at_limit) is left to the caller (joint_obs per dof)
 template <typename T>
 __device__ inline void calc_state(const T* st, const double* wt, float* obs42, float* joint_speeds, int& joints_at_limit,
-                                  PostPhys<T>& pp, const T* scs = nullptr) {
+                                  PostPhys<T>& pp, const T* scs = nullptr, bool joints = true) {
     Kin<T> K;
     if (scs) forward_kinematics_pre(st + 3, scs, K);   // hinge sin / cos of this state precomputed across lanes
     else forward_kinematics(st + 3, st + 13, K);
@@ -146,19 +159,18 @@ __device__ inline void calc_state(const T* st, const double* wt, float* obs42, f
     pp.rfoot[1] = bpy + (double)parts[PART_RIGHT_FOOT][1];
     double qd4[4] = {(double)st[3], (double)st[4], (double)st[5], (double)st[6]};
     euler_from_quat(qd4, pp.roll, pp.pitch, pp.yaw);
-    joints_at_limit = 0;
+    if (joints) joints_at_limit = 0;
 #pragma unroll
     for (int i = 0; i < NDOF; i++) {
         pp.q[i] = (double)st[13 + i];
         pp.qd[i] = (double)st[30 + i];
-        const double lo = dof_lo[i], hi = dof_hi[i];
-        const double mid = 0.5 * (lo + hi);
-        const float rp = (float)(2 * (pp.q[i] - mid) / (hi - lo));
-        const float rv = (float)(pp.qd[i] * 0.1);
-        obs42[8 + 2 * i] = rp;
-        obs42[9 + 2 * i] = rv;
-        joint_speeds[i] = rv;
-        if (fabsf(rp) > 0.99f) joints_at_limit++;
+        if (joints) {
+            float rp, rv;
+            if (joint_obs(st, i, rp, rv)) joints_at_limit++;
+            obs42[8 + 2 * i] = rp;
+            obs42[9 + 2 * i] = rv;
+            joint_speeds[i] = rv;
+        }
     }
 #pragma unroll
     for (int i = 0; i < 3; i++) pp.lin[i] = (double)st[7 + i];
@@ -177,7 +189,7 @@ __device__ inline void calc_state(const T* st, const double* wt, float* obs42, f
     obs42[6] = (float)pp.roll;
     obs42[7] = (float)pp.pitch;
 #pragma unroll
-    for (int i = 0; i < 42; i++) obs42[i] = fminf(fmaxf(obs42[i], -5.0f), 5.0f);
+    for (int i = 0; i < (joints ? 42 : 8); i++) obs42[i] = fminf(fmaxf(obs42[i], -5.0f), 5.0f);
 }
 
 // getLowLevelObs tail (low_level_env.py:307-320): 14 x (relative target, target velocity) at `frame`

@@ -253,15 +253,21 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
                                                           unsigned& ef, const T* scs = nullptr,
                                                           bool* defer_reset = nullptr,   // the caller runs the
                                                                                          // auto-reset and the store
-                                                          float* obs_dst = nullptr) {    // obs row (default: a.obs)
+                                                          float* obs_dst = nullptr,      // obs row (default: a.obs)
+                                                          const float* js_pre = nullptr,  // the joint block done by
+                                                          int jal_pre = 0) {              // the env's lanes (obs_dst)
     // i: the lane (state, bookkeeping); io: its output row of this step (t * n + i, hum_step_k)
     const ClipDev& c = a.clips[b.clip];
     float obs[HUM_NOBS];
     // calc_state (:481) and robot_pos (:483-486)
     float js[NDOF];
-    int jal;
+    int jal = jal_pre;
     PostPhys<T> pp;
-    calc_state(st, b.wt, obs, js, jal, pp, scs);
+    calc_state(st, b.wt, obs, js, jal, pp, scs, js_pre == nullptr);
+    if (js_pre) {
+#pragma unroll
+        for (int k = 0; k < NDOF; k++) js[k] = js_pre[k];
+    }
     SUBPHASE(19);
     b.robot_pos[0] = pp.bx; b.robot_pos[1] = pp.by; b.robot_pos[2] = 0;
     // updateReward (:441-465)
@@ -331,7 +337,8 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
     SUBPHASE(22);
     float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
 #pragma unroll
-    for (int k = 0; k < HUM_NOBS; k++) orow[k] = obs[k];
+    for (int k = 0; k < HUM_NOBS; k++)
+        if (!js_pre || k < 8 || k >= 42) orow[k] = obs[k];
     SUBPHASE(16);
     a.rew[io] = (float)total;
     a.done[io] = done ? 1 : 0;
@@ -940,6 +947,23 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         rstage[l] = pact0;
         if (l == 0) rstage[GL] = pact1;
     }
+    // low-level env: calc_state's joint block (obs 8..41, the joint speeds, the at-limit count) one dof per lane, into
+    // the staging row (clamped like the observation) and the joint speeds past the reset obs row
+    float* jstage = reinterpret_cast<float*>(scs + 216);
+    static_assert(sizeof(sh[0].x.aba.IA) >= (216 + NDOF) * sizeof(T), "joint speed staging");
+    int jal_l = 0;
+    if (!a.hier) {
+        unsigned jmask = 0;
+        for (int d = l; d < NDOF; d += GL) {
+            float rp, rv;
+            if (joint_obs(S.st, d, rp, rv)) jmask |= 1u << (d / GL);
+            ostage[8 + 2 * d] = fminf(fmaxf(rp, -5.0f), 5.0f);
+            ostage[9 + 2 * d] = fminf(fmaxf(rv, -5.0f), 5.0f);
+            jstage[d] = rv;
+        }
+        const unsigned long long b0 = __ballot(jmask & 1u), b1 = __ballot((jmask >> 1) & 1u);
+        jal_l = __popcll((b0 >> gbit) & 0xFFFFull) + __popcll((b1 >> gbit) & 0xFFFFull);
+    }
     wave_sync();
     PHASE_INIT;
     Book b;
@@ -967,7 +991,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
                 float act[HUM_NACT];
 #pragma unroll
                 for (int k = 0; k < HUM_NACT; k++) act[k] = POLICY ? rstage[k] : a.act[io * HUM_NACT + k];
-                post_step(a, i, io, st, b, act, ef, scs, &rst, ostage);
+                post_step(a, i, io, st, b, act, ef, scs, &rst, ostage, jstage, jal_l);
             }
         }
     }
