@@ -170,6 +170,19 @@ constexpr LinkInfo link_info() {
 constexpr LinkInfo LINKS = link_info();
 __device__ inline int body_nlink_l(int b) { return (int)((pack_bits<2>(LINKS.nlink) >> (2 * b)) & 3u); }
 __device__ inline int body_link0_l(int b) { return (int)((pack_bits<4>(LINKS.link0) >> (4 * b)) & 15u); }
+struct DofBodies { int b[NDOF]; };
+constexpr DofBodies dof_bodies() {
+    DofBodies r{};
+    for (int x = 0; x < NB; x++)
+        for (int k = 0; k < body_ndof[x]; k++) r.b[body_dof0[x] + k] = x;
+    return r;
+}
+constexpr DofBodies DOFB = dof_bodies();
+static_assert(NB <= 16 && NDOF <= 32, "4-bit body codes, two constants");
+constexpr unsigned long long DOFB_LO = pack_bits<4>(DOFB.b), DOFB_HI = pack_bits<4>(DOFB.b, 16);
+__device__ inline int dof_body_l(int d) {   // the body dof d moves: d < 16 from one constant, d >= 16 the other
+    return d < 16 ? (int)((DOFB_LO >> (4 * (d & 15))) & 15u) : (int)((DOFB_HI >> (4 * (d - 16))) & 15u);
+}
 __device__ inline int geom_body_l(int g) {   // g < 16 from one constant, g = 16 the other
     return g < 16 ? (int)((pack_bits<4>(geom_body) >> (4 * (g & 15))) & 15u) : geom_body[16];
 }
@@ -1191,18 +1204,21 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 for (int i = 0; i < 3; i++) S.o[b][i] = K.o[b][i];
             }
 #pragma unroll
-            for (int b = 1; b < NB; b++)
+            for (int d = 0; d < NDOF; d++)   // the hinge axes: the first half of the motion subspace columns
 #pragma unroll
-                for (int k = 0; k < body_ndof[b]; k++) {   // motion subspace columns [u; o_b x u]
-                    const int d = body_dof0[b] + k;
-#pragma unroll
-                    for (int i = 0; i < 3; i++) S.Sc[d][i] = K.u[d][i];
-                    cross3(K.o[b], K.u[d], S.Sc[d] + 3);
-                }
+                for (int i = 0; i < 3; i++) S.Sc[d][i] = K.u[d][i];
         }
         if (l < 16) {   // generalised velocity
             S.nu[l] = l < 3 ? S.st[10 + l] : (l < 6 ? S.st[7 + l - 3] : S.st[30 + l - 6]);
             if (l < NV - 16) S.nu[16 + l] = S.st[30 + 10 + l];
+        }
+        wave_sync();
+        for (int d = l; d < NDOF; d += GL) {   // motion subspace columns [u; o_b x u], one dof per lane
+            const int b = dof_body_l(d);
+            T ob[3], u[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) { ob[i] = S.o[b][i]; u[i] = S.Sc[d][i]; }
+            cross3(ob, u, S.Sc[d] + 3);
         }
     }
     __syncthreads();
