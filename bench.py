@@ -401,8 +401,9 @@ def main():
             "vs_baseline": None, "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
             "config": {"workload": ("HumanoidBulletEnv-v0-Hier two-level rollout (high heading every 5 low steps), "
                                     if a.hier else "HumanoidBulletEnv-v0-Low step+reward, ") +
-                                   "%s, %d envs/GPU, %s, auto-reset, %d env steps per %s" % (
-                                       a.clip, n, _actions_desc(a), a.k,
+                                   "%s, %d envs/GPU, %s, auto-reset, %s env steps per %s" % (
+                                       a.clip, n, _actions_desc(a),
+                                       "/".join(str(s) for s in sorted(set(sizes), reverse=True)),
                                        "hum_hier_rollout call (2 policy launches + 1 env launch per transition)"
                                        if a.hier and a.policy else "launch"),
                        "fused": bool(a.policy and a.fused and not a.hier),
