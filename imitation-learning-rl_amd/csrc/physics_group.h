@@ -1686,12 +1686,14 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             T lnA = T(0), lnB = T(0), lnC = T(0), lnD;
             // P of the row being solved, from its reduction one stage earlier (the first row's here)
             T pA = fma(A.meff, A.b - row_sum(A.j0 * n0 + A.j1 * n1), A.lam), pB, pC, pD, dlp = T(0);
-            // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read
-            auto stage = [&](auto masked, int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, int oX, int& oW, T pX,
-                             T& pY, T lnX, T& lnW) {
+            // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read; Z is row k+2
+            auto stage = [&](auto masked, int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, const RowRegs& Z, int oX,
+                             int& oW, T pX, T& pY, T lnX, T& lnW) {
                 oW = X.next3;
                 load(oW, W);
                 lnW = load_ln(X.next3_ln);
+                // the row-ahead loads issue at the top of their stage: ALU work may cross this point, LDS ops may not
+                __builtin_amdgcn_sched_barrier(0x407);
                 pY = fma(Y.meff, Y.b - row_sum(Y.j0 * n0 + Y.j1 * n1), Y.lam);
                 const T lo = -(X.mu * lnX), hi = X.hi + X.mu * lnX;
                 const T tX = fma(-X.q, dlp, pX);
@@ -1706,17 +1708,18 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 n0 = fma(X.m0, dl, n0);
                 n1 += X.m1 * dl;
                 dlp = dl;
-                // the row read this stage must have landed by its end: keeps the scheduler from sinking its loads
-                // next to their first use two stages on, where the LDS latency was exposed (+1.1 %,
+                // the row read one stage earlier (Z) must have landed by the end of this one: keeps the scheduler
+                // from sinking its loads next to their first use, where the LDS latency was exposed (+1.1 %), and
+                // gives them a whole stage to land (pinning the row read in this stage instead, with the loads at
+                // the stage top: -0.4 %; every field of the row and its bounding lambda pinned: no change;
                 // profiles/r04_ab_rows.txt)
-                // (pinning every field of the row and its bounding lambda as well measured the same)
-                asm volatile("" ::"v"(W.j0), "v"(W.m0), "v"(W.j1), "v"(W.m1), "v"(W.b), "v"(W.meff));
+                asm volatile("" ::"v"(Z.j0), "v"(Z.m0), "v"(Z.j1), "v"(Z.m1), "v"(Z.b), "v"(Z.meff));
             };
             auto round = [&](auto masked, int k) {
-                stage(masked, k, A, B, D, oA, oD, pA, pB, lnA, lnD);
-                stage(masked, k + 1, B, C, A, oB, oA, pB, pC, lnB, lnA);
-                stage(masked, k + 2, C, D, B, oC, oB, pC, pD, lnC, lnB);
-                stage(masked, k + 3, D, A, C, oD, oC, pD, pA, lnD, lnC);
+                stage(masked, k, A, B, D, C, oA, oD, pA, pB, lnA, lnD);
+                stage(masked, k + 1, B, C, A, D, oB, oA, pB, pC, lnB, lnA);
+                stage(masked, k + 2, C, D, B, A, oC, oB, pC, pD, lnC, lnB);
+                stage(masked, k + 3, D, A, C, B, oD, oC, pD, pA, lnD, lnC);
             };
             int k = 0;
             // two rounds per iteration: the scheduler sinks a round's last row-ahead loads to the loop end, where the
