@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--gather-every", type=int, default=0,
                     help="multi-GPU: trajectory all-gather of the last G env steps every G env steps (G %% k == 0)")
     ap.add_argument("--k", type=int, default=K_DEFAULT, help="env steps per launch (hum_step_k)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed and run every collective (barriers, the timing all-reduce, the "
+                         "gather) even with one rank: the RCCL code path on a one-GPU box, where RCCL refuses two ranks "
+                         "on one device")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: host-staged, tests)")
     ap.add_argument("--dump-gather", default=None,
@@ -268,7 +272,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             if kk < k:
                 rem_out[kk] = env.step_k_out(kk)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if a.dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     stream = torch.cuda.current_stream(dev)
@@ -277,7 +281,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     ev0.record(stream)
     for s in range(launches):
         step(s, sizes[s])
-        if G and world > 1 and not a.policy and ((s + 1) * k) % G == 0:
+        if G and a.dist and not a.policy and ((s + 1) * k) % G == 0:
             tg = time.perf_counter()
             frag = _fragment(a, ring, [pool[(s - j) % 16] for j in range(len(ring) - 1, -1, -1)])
             from ilrl_amd.parallel import gather_trajectories
@@ -287,19 +291,19 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             gather_s += time.perf_counter() - tg
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if a.dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / steps   # per env step, on the launch stream (torch's current)
-    wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if world > 1 else wall
+    wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if a.dist else wall
     low_steps = None
     if a.hier and a.policy:   # physics env-steps in the timed region: the low-level transitions the rollouts recorded
         from ilrl_amd import _native as N
         low_steps = float(sum(int((x == N.HUM_AGENT_LOW).sum().item()) for x in env._bench_acted[wlaunches:]))
     elif a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
         low_steps = float(count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank))
-        if world > 1:
+        if a.dist:
             low_steps = _all_reduce(world, dev, a.backend, low_steps, dist.ReduceOp.SUM)   # all ranks
     return env, wall, kern_ms, low_steps, gather_s, gathered, sizes
 
@@ -352,11 +356,12 @@ def main():
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    a.dist = world > 1 or a.force_dist
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; ranks beyond the visible devices share them (tests on a one-GPU box)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    if world > 1:
+    if a.dist:
         torch.cuda.set_device(dev)
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -429,7 +434,7 @@ def main():
             out["unit"] = "env-steps/s"
             out["physics_env_steps_per_step"] = phys_steps_per_step
             out["agent_transitions_per_s"] = total / wall_max
-        if world > 1 and a.gather_every:
+        if a.dist and a.gather_every:
             out["gather"] = {"every": a.gather_every, "seconds": gather_s, "backend": a.backend,
                              "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1), "fragments": len(gathered) or None}
         if world == 1 and not a.no_secondary and not a.hier and not a.policy:
@@ -454,7 +459,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds, a.cpu_workers or host_cores())
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if a.dist:
         dist.destroy_process_group()
 
 

@@ -30,8 +30,9 @@ def gather_trajectories(tensors, dst=0):
     All buffers are packed, row by row, into ONE uint8 message (their raw bytes: int64 / uint8 / float keep
     their exact values), so RCCL moves one large payload per call: xGMI is point-to-point, so few large
     collectives beat many small ones.  Returns the list on dst, None elsewhere."""
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
+    on = dist.is_initialized()   # one rank with the group initialised still runs the collectives (bench --force-dist)
+    world = dist.get_world_size() if on else 1
+    rank = dist.get_rank() if on else 0
     n = int(tensors[0].shape[0])
     if any(int(t.shape[0]) != n for t in tensors):
         raise ValueError("every buffer needs the same leading (lane) dimension")
@@ -39,9 +40,9 @@ def gather_trajectories(tensors, dst=0):
     widths = [_row_bytes(t) for t in tensors]
     flat = torch.cat([t.contiguous().reshape(n, -1).view(torch.uint8).reshape(n, w) for t, w in zip(tensors, widths)],
                      dim=1) if n else torch.zeros((0, sum(widths)), dtype=torch.uint8, device=dev)
-    if world > 1 and dist.get_backend() == "gloo" and flat.is_cuda:   # gloo gathers host tensors
+    if on and dist.get_backend() == "gloo" and flat.is_cuda:   # gloo gathers host tensors
         flat, dev = flat.cpu(), torch.device("cpu")
-    if world == 1:
+    if not on:
         full, counts = flat, [n]
     else:
         cnt = torch.tensor([n], dtype=torch.int64, device=dev)

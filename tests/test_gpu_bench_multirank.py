@@ -1,8 +1,11 @@
 """Config 4's real benchmark path (BASELINE.json configs[3]: lanes sharded over ranks, trajectory gather to the
 learner rank) end to end on the one-GPU box: bench.py under torch.distributed.run (every rank on cuda:0, gloo -
-RCCL needs one GPU per rank; the 8-GPU RCCL/xGMI run is the driver's).  Two shapes: 2 ranks x 2048 lanes, 8 env
+RCCL needs one GPU per rank; the 8-GPU RCCL/xGMI run is the driver's).  Three runs: 2 ranks x 2048 lanes, 8 env
 steps per launch, a gather every 8 env steps; and config 4's own shape, 8 ranks x 4096 lanes = 32,768 lanes, 32 env
-steps per launch (the bench default) and a gather every 32 env steps.  Rank 0's gathered obs / action / reward /
+steps per launch (the bench default) and a gather every 32 env steps; and the RCCL ("nccl") path itself - RCCL
+refuses two ranks on one device ("Duplicate GPU detected", profiles/r04_rccl_probe.txt), so one rank with
+--force-dist runs the process group, barriers, the device-tensor timing all-reduce and the all_gather_into_tensor
+gather through RCCL.  Rank 0's gathered obs / action / reward /
 done fragments must equal those of ONE handle over all the lanes stepped with the same actions, bit for bit (every
 lane's RNG stream is keyed by its global id); at 32,768 lanes rank 0 keeps every 61st lane of the
 fragment (all eight shards are sampled) to bound host memory."""
@@ -35,17 +38,20 @@ def _port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("ranks,lanes,k,every,steps,stride", [(2, 2048, 8, 8, 16, 1), (8, 4096, 32, 32, 32, 61)],
-                         ids=["2x2048", "config4_8x4096"])
-def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride):
+@pytest.mark.parametrize("ranks,lanes,k,every,steps,stride,backend",
+                         [(2, 2048, 8, 8, 16, 1, "gloo"), (8, 4096, 32, 32, 32, 61, "gloo"), (1, 4096, 32, 32, 64, 7, "nccl")],
+                         ids=["2x2048", "config4_8x4096", "rccl_1x4096"])
+def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride, backend):
     import types
     sys.path.insert(0, REPO)
     import bench
     dump = str(tmp_path / "gather.npz")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(ranks),
-           "--backend", "gloo", "--lanes", str(lanes), "--steps", str(steps), "--warmup", "0", "--k", str(k),
+           "--backend", backend, "--lanes", str(lanes), "--steps", str(steps), "--warmup", "0", "--k", str(k),
            "--gather-every", str(every), "--dump-gather", dump, "--dump-lane-stride", str(stride), "--cpu-seconds", "0"]
+    if ranks == 1:   # RCCL refuses two ranks on one device: one rank with every collective run through it
+        cmd += ["--force-dist", "--no-secondary"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=560, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -54,6 +60,7 @@ def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, ever
     assert line["n_gpus"] == ranks and line["config"]["steps_per_launch"] == [k]
     assert line["config"]["launches"] == steps // k
     assert line["gather"]["every"] == every and line["gather"]["fragments"] == steps // every
+    assert line["gather"]["backend"] == backend
     assert line["value"] > 0 and line["error_flags"] == 0
     g = np.load(dump)
     total = ranks * lanes
