@@ -2,7 +2,7 @@
 //
 // MI355X mapping: a 64-lane wavefront = 4 envs x 16 lanes; each env's working set lives in LDS
 // (struct GroupLDS, ~10 KB fp32), so a CU holds 16 envs (4 blocks of one wave: one wave per SIMD, the CU's
-// 160 KB; the kernel holds 512 VGPRs and spills 25 of them, 80 B of scratch per lane, tests/test_cpu_isa.py).
+// 160 KB; the kernel holds 512 VGPRs and spills 16 of them, 68 B of scratch per lane, tests/test_cpu_isa.py).
 // Same algorithm and operation order as physics.h (the per-lane kernel,
 // kept as the reference-shaped variant) except for the order of floating-point sums inside the
 // element-parallel ABA backward pass and the 16-lane DPP reductions of the PGS row products.
@@ -1401,12 +1401,24 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     PHASE(4);
     // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
     auto& C = S.x.cr;
+    // the broad phase's per-geom inputs (endpoint sum, bounding radius) in the row storage the rows phase has not
+    // written yet (the survivor list sits two rows above): each pair test reads two 4-wide entries
+    T* gsum = &C.row[MAXR_LDS - 5][0];
+    static_assert(2 * RW >= 4 * NGEOM && MAXR_LDS >= 5, "two rows hold the broad-phase geom table");
     for (int g = l; g < NGEOM; g += GL) {
         const int b = geom_body_l(g);
+        T e0[3], e1[3];
 #pragma unroll
         for (int i = 0; i < 3; i++) {
-            C.gp[g][0][i] = S.o[b][i] + S.R[b][3 * i] * M.gp1[g][0] + S.R[b][3 * i + 1] * M.gp1[g][1] + S.R[b][3 * i + 2] * M.gp1[g][2];
-            C.gp[g][1][i] = S.o[b][i] + S.R[b][3 * i] * M.gp2[g][0] + S.R[b][3 * i + 1] * M.gp2[g][1] + S.R[b][3 * i + 2] * M.gp2[g][2];
+            e0[i] = S.o[b][i] + S.R[b][3 * i] * M.gp1[g][0] + S.R[b][3 * i + 1] * M.gp1[g][1] + S.R[b][3 * i + 2] * M.gp1[g][2];
+            e1[i] = S.o[b][i] + S.R[b][3 * i] * M.gp2[g][0] + S.R[b][3 * i + 1] * M.gp2[g][1] + S.R[b][3 * i + 2] * M.gp2[g][2];
+            C.gp[g][0][i] = e0[i];
+            C.gp[g][1][i] = e1[i];
+        }
+        if (P.self_collision) {
+#pragma unroll
+            for (int i = 0; i < 3; i++) gsum[4 * g + i] = e0[i] + e1[i];
+            gsum[4 * g + 3] = geom_br_l<T>(g);
         }
     }
     const int gbit = (threadIdx.x & 63) & ~(GL - 1);   // first lane of this group in the wave
@@ -1524,10 +1536,19 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             bool maybe = false;
             if (pd != 0xffff) {
                 const int ga = pd & 31, gb = pd >> 5;
-                T dm[3];
+                T qa[4], qb[4], dm[3];
+                if constexpr (sizeof(T) == 4) {
+                    using f4v = float __attribute__((ext_vector_type(4)));
+                    const f4v va = *reinterpret_cast<const f4v*>(gsum + 4 * ga), vb = *reinterpret_cast<const f4v*>(gsum + 4 * gb);
+                    qa[0] = va.x; qa[1] = va.y; qa[2] = va.z; qa[3] = va.w;
+                    qb[0] = vb.x; qb[1] = vb.y; qb[2] = vb.z; qb[3] = vb.w;
+                } else {
 #pragma unroll
-                for (int i = 0; i < 3; i++) dm[i] = (C.gp[ga][0][i] + C.gp[ga][1][i]) - (C.gp[gb][0][i] + C.gp[gb][1][i]);
-                const T rr = geom_br_l<T>(ga) + geom_br_l<T>(gb) + reach;
+                    for (int i = 0; i < 4; i++) { qa[i] = gsum[4 * ga + i]; qb[i] = gsum[4 * gb + i]; }
+                }
+#pragma unroll
+                for (int i = 0; i < 3; i++) dm[i] = qa[i] - qb[i];   // (pa1 + pa2) - (pb1 + pb2)
+                const T rr = qa[3] + qb[3] + reach;
                 maybe = dot3(dm, dm) < T(4) * rr * rr;   // |ma - mb| < rr with ma = (p1 + p2) / 2
             }
             const unsigned long long bm = (__ballot(maybe) >> gbit) & 0xFFFFull;
