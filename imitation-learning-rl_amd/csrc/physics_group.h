@@ -2,7 +2,7 @@
 //
 // MI355X mapping: a 64-lane wavefront = 4 envs x 16 lanes; each env's working set lives in LDS
 // (struct GroupLDS, ~10 KB fp32), so a CU holds 16 envs (4 blocks of one wave: one wave per SIMD, the CU's
-// 160 KB; the kernel holds 512 VGPRs and spills 16 of them, 68 B of scratch per lane, tests/test_cpu_isa.py).
+// 160 KB; the kernel holds 512 VGPRs and spills 30 of them, 84 B of scratch per lane, tests/test_cpu_isa.py).
 // Same algorithm and operation order as physics.h (the per-lane kernel,
 // kept as the reference-shaped variant) except for the order of floating-point sums inside the
 // element-parallel ABA backward pass and the 16-lane DPP reductions of the PGS row products.
@@ -1401,10 +1401,12 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     PHASE(4);
     // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
     auto& C = S.x.cr;
-    // the broad phase's per-geom inputs (endpoint sum, bounding radius) in the row storage the rows phase has not
-    // written yet (the survivor list sits two rows above): each pair test reads two 4-wide entries
-    T* gsum = &C.row[MAXR_LDS - 5][0];
-    static_assert(2 * RW >= 4 * NGEOM && MAXR_LDS >= 5, "two rows hold the broad-phase geom table");
+    // per-geom table for the contact phase, in the row storage the rows phase has not written yet (the survivor
+    // list sits two rows above): endpoint sum and bounding radius (the broad phase's pair test reads two such
+    // quads), then radius and body (ground points, narrow phase) - LDS reads instead of per-lane selects among
+    // compile-time constants
+    T* gsum = &C.row[MAXR_LDS - 6][0];
+    static_assert(3 * RW >= 8 * NGEOM && MAXR_LDS >= 6, "three rows hold the contact phase's geom table");
     for (int g = l; g < NGEOM; g += GL) {
         const int b = geom_body_l(g);
         T e0[3], e1[3];
@@ -1415,11 +1417,11 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             C.gp[g][0][i] = e0[i];
             C.gp[g][1][i] = e1[i];
         }
-        if (P.self_collision) {
 #pragma unroll
-            for (int i = 0; i < 3; i++) gsum[4 * g + i] = e0[i] + e1[i];
-            gsum[4 * g + 3] = geom_br_l<T>(g);
-        }
+        for (int i = 0; i < 3; i++) gsum[8 * g + i] = e0[i] + e1[i];
+        gsum[8 * g + 3] = geom_br_l<T>(g);
+        gsum[8 * g + 4] = geom_r_l<T>(g);
+        gsum[8 * g + 5] = (T)b;
     }
     const int gbit = (threadIdx.x & 63) & ~(GL - 1);   // first lane of this group in the wave
     const unsigned long long lanemask_lt = (1ull << (threadIdx.x & 63)) - 1ull;
@@ -1493,7 +1495,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
             if (gd != 0xffff) {
                 const int ga = gd & 31, e = (gd >> 5) & 1;
-                const T gr = geom_r_l<T>(ga);
+                const T gr = gsum[8 * ga + 4];
                 const T* p = C.gp[ga][e];
                 d = basez + p[2] - gr;
                 hit = d < (T)P.contact_thresh;
@@ -1513,7 +1515,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
             if (gd != 0xffff) {
                 const int ga = gd & 31, e = (gd >> 5) & 1;
-                const T gr = geom_r_l<T>(ga);
+                const T gr = gsum[8 * ga + 4];
                 const T* p = C.gp[ga][e];
                 const T cw[3] = {S.st[0] + p[0], S.st[1] + p[1], basez + p[2]};
                 hit = terrain_contact<T>(P, tkey, cw, gr, n, d);
@@ -1539,12 +1541,12 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 T qa[4], qb[4], dm[3];
                 if constexpr (sizeof(T) == 4) {
                     using f4v = float __attribute__((ext_vector_type(4)));
-                    const f4v va = *reinterpret_cast<const f4v*>(gsum + 4 * ga), vb = *reinterpret_cast<const f4v*>(gsum + 4 * gb);
+                    const f4v va = *reinterpret_cast<const f4v*>(gsum + 8 * ga), vb = *reinterpret_cast<const f4v*>(gsum + 8 * gb);
                     qa[0] = va.x; qa[1] = va.y; qa[2] = va.z; qa[3] = va.w;
                     qb[0] = vb.x; qb[1] = vb.y; qb[2] = vb.z; qb[3] = vb.w;
                 } else {
 #pragma unroll
-                    for (int i = 0; i < 4; i++) { qa[i] = gsum[4 * ga + i]; qb[i] = gsum[4 * gb + i]; }
+                    for (int i = 0; i < 4; i++) { qa[i] = gsum[8 * ga + i]; qb[i] = gsum[8 * gb + i]; }
                 }
 #pragma unroll
                 for (int i = 0; i < 3; i++) dm[i] = qa[i] - qb[i];   // (pa1 + pa2) - (pb1 + pb2)
@@ -1572,7 +1574,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #pragma unroll
                 for (int i = 0; i < 3; i++) dv[i] = ca[i] - cb[i];
                 const T dist = psqrt(dot3(dv, dv));
-                const T ra = geom_r_l<T>(ga), rb = geom_r_l<T>(gb);
+                const T ra = gsum[8 * ga + 4], rb = gsum[8 * gb + 4];
                 d = dist - ra - rb;
                 hit = d < (T)P.contact_thresh && dist > (T)1e-9;
                 if (hit) {
@@ -1584,8 +1586,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                         pb[i] = cb[i] + rb * n[i];
                     }
                 }
-                ba = geom_body_l(ga);
-                bb = geom_body_l(gb);
+                ba = (int)gsum[8 * ga + 5];
+                bb = (int)gsum[8 * gb + 5];
             }
             emit(hit, ba, bb, pa, pb, n, d);
         }
