@@ -701,12 +701,12 @@ __device__ inline void g_row_jacobian2(const GroupLDS<T>& S, int ba, const T* fa
 // per-env counts are wave-uniform (readlane), so the env/row of a task is two compares away.
 template <typename T>
 __device__ __attribute__((always_inline)) void store_row(T* R, const T* J, const T* Mi, const T* sc, int next3,
-                                                         int next3_ln) {
+                                                         int next3_ln, T qc = T(0)) {
 #pragma unroll
     for (int q = 0; q < NV; q++) { R[2 * q] = J[q]; R[2 * q + 1] = Mi[q]; }
     R[RO_Z] = T(0); R[RO_Z + 1] = T(0);
     R[RO_S0] = sc[0]; R[RO_S0 + 1] = sc[2]; R[RO_S0 + 2] = sc[3]; R[RO_S0 + 3] = sc[4];
-    R[RO_S1] = sc[5]; R[RO_S1 + 1] = T(0);   // c: filled by group_couplings
+    R[RO_S1] = sc[5]; R[RO_S1 + 1] = qc;   // q = meff c (0 after a zero row; else from group_rows)
     *reinterpret_cast<int*>(R + RO_S1 + 2) = next3;
     *reinterpret_cast<int*>(R + RO_S1 + 3) = next3_ln;
 }
@@ -871,18 +871,44 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         sc[3] = 0;
         sc[4] = prcp(jm);
         const int p = epos + pool_pos(r, enl, enc);
+        // coupling c_r = J_r . (M^-1 J^T)_pred(r) from the lane that solved the predecessor row in this round
+        // (ds_bpermute); predecessors in another round are left to the LDS pass below
+        T qc = T(0);
+        {
+            const int qr = p - epos, qp = qr == 0 ? pool_rows(enl, enc) - 1 : qr - 1;
+            const int rp = qp < enl + enc ? qp : qp - pool_gap(enc);
+            const int tp = (t - r) + rp, t0 = t - lane;
+            const bool here = !pool_zero(qp, enl, enc) && tp >= t0 && tp < t0 + EPB_ * GL;
+            const int src = 4 * (here ? tp - t0 : lane);
+            T c = 0;
+#pragma unroll
+            for (int q = 0; q < NV; q++) {
+                T mp;
+                if constexpr (sizeof(T) == 4) {
+                    mp = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(Mi[q])));
+                } else {
+                    const long long b = __double_as_longlong(Mi[q]);
+                    const int lo = __builtin_amdgcn_ds_bpermute(src, (int)(b & 0xffffffff));
+                    const int hi = __builtin_amdgcn_ds_bpermute(src, (int)(b >> 32));
+                    mp = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+                }
+                c += J[q] * mp;
+            }
+            if (here) qc = c * sc[4];
+        }
         if (p < cap) {
             int n3, n3ln;
             pgs_link<T>(epos, p - epos, enl, enc, n3, n3ln);   // (used only when all of the block's rows are in LDS)
-            store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, n3, n3ln);
+            store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, n3, n3ln, qc);
         }
         else {
             store_row_global(gblock + (long)(p - cap) * RW, J, Mi, sc);
         }
     }
     // couplings c_r = J_r . (M^-1 J^T)_pred(r) (cyclic predecessor; 0 after a zero row) for the lookahead
-    // PGS, which needs them only when the block's rows all sit in LDS
-    if (pos[EPB_] <= cap) {
+    // PGS, which needs them only when the block's rows all sit in LDS: the rows whose predecessor another round
+    // solved (more rows than lanes), from LDS
+    if (pos[EPB_] <= cap && total > EPB_ * GL) {   // rows whose predecessor was solved in another round
         wave_sync();
         for (int t = lane; t < total; t += EPB_ * GL) {
             int e = 0;
@@ -894,7 +920,8 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 if (q == e) { r = t - pre[q]; epos = pos[q]; enl = nls[q]; enc = ncs[q]; }
             const int qr = pool_pos(r, enl, enc);
             const int qp = qr == 0 ? pool_rows(enl, enc) - 1 : qr - 1;
-            if (!pool_zero(qp, enl, enc)) {
+            const int tp = (t - r) + (qp < enl + enc ? qp : qp - pool_gap(enc));
+            if (!pool_zero(qp, enl, enc) && tp / (EPB_ * GL) != t / (EPB_ * GL)) {
                 T* Rr = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(epos + qr));
                 const T* Rp = reinterpret_cast<const T*>(reinterpret_cast<const char*>(shb) + pool_off<T>(epos + qp));
                 T c = 0;
