@@ -1007,9 +1007,13 @@ __device__ __attribute__((always_inline)) void aba_load(const GroupLDS<T>& S, co
     }
 }
 
+// Levels 1 and 3 take their first (level 3: only) child's contribution from registers: that child is the body the same
+// lane group updated one level earlier (kIA / kpa, the previous call's oIA / opa); levels 0 and 2 need not store theirs.
 template <typename T, int LV>
 __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt,
-                                                               const AbaIn<T>& in) {
+                                                               const AbaIn<T>& in, const T* kIA, const T* kpa, T* oIA,
+                                                               T* opa) {
+    constexpr bool KREG = LV == 1 || LV == 3, STORE = LV == 1 || LV == 3;
     auto& A = S.x.aba;
     constexpr int KM = aba_km<LV>();
     const int b = lvl_sel<LV>(g, [](int x) { return x; });
@@ -1027,7 +1031,15 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
         for (int e = 0; e < 6; e++) pAb[e] += A.pA[kid][e];
     };
     // every group of a level has the same number of kids (0, 1 or 2)
-    if constexpr (LVL_KID[LV][0][0] >= 0)
+    static_assert(!KREG || (LVL_KID[LV][0][0] == LVL_BODY[LV - 1][0] && LVL_KID[LV][1][0] == LVL_BODY[LV - 1][1] &&
+                            LVL_KID[LV][2][0] == LVL_BODY[LV - 1][2] && LVL_KID[LV][3][0] == LVL_BODY[LV - 1][3]),
+                  "a register child is the body the same group updated one level earlier");
+    if constexpr (KREG) {
+#pragma unroll
+        for (int q = 0; q < 21; q++) IA[q] += kIA[q];
+#pragma unroll
+        for (int e = 0; e < 6; e++) pAb[e] += kpa[e];
+    } else if constexpr (LVL_KID[LV][0][0] >= 0)
         add_kid(g == 0 ? LVL_KID[LV][0][0] : (g == 1 ? LVL_KID[LV][1][0] : (g == 2 ? LVL_KID[LV][2][0] : LVL_KID[LV][3][0])));
     if constexpr (LVL_KID[LV][0][1] >= 0)
         add_kid(g == 0 ? LVL_KID[LV][0][1] : (g == 1 ? LVL_KID[LV][1][1] : (g == 2 ? LVL_KID[LV][2][1] : LVL_KID[LV][3][1])));
@@ -1091,9 +1103,15 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
     // contribution to the parent in the body's own (now dead) slots; factorisation for passes 3 / responses.
     // The 4 lanes of a group (and groups sharing a body) write identical values.
 #pragma unroll
-    for (int q = 0; q < 21; q++) A.IA[b][q] = IA[q];
+    for (int q = 0; q < 21; q++) {
+        oIA[q] = IA[q];
+        if constexpr (STORE) A.IA[b][q] = IA[q];
+    }
 #pragma unroll
-    for (int e = 0; e < 6; e++) A.pA[b][e] = pa[e];
+    for (int e = 0; e < 6; e++) {
+        opa[e] = pa[e];
+        if constexpr (STORE) A.pA[b][e] = pa[e];
+    }
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         if (j < k) {
@@ -1152,9 +1170,21 @@ __device__ __attribute__((always_inline)) void fwd_load(const GroupLDS<T>& S, co
         for (int i = 0; i < KM; i++) in.Dinv[3 * i + j] = i < k && j < k ? S.Dinv[doff + k * i + j] : T(0);   // padded: 0
     }
 }
+// Levels 0, 1 and 3 take the parent's acceleration and velocity from registers (pa / pv): the base (computed on every
+// lane) or the body the same lane group solved one level earlier; level 2's pelvis children read them from LDS.
+template <int LV>
+constexpr bool fwd_parent_in_regs() {
+    if (LV == 2) return false;
+    for (int i = 0; i < 4; i++)
+        if (body_parent[FWD_BODY[LV][i]] != (LV == 0 ? 0 : FWD_BODY[LV - 1][i])) return false;
+    return true;
+}
 template <typename T, int LV>
 __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt,
-                                                               const FwdIn<T>& in) {
+                                                               const FwdIn<T>& in, const T* pa, const T* pv, T* oa,
+                                                               T* ov) {
+    constexpr bool PREG = LV != 2;
+    static_assert(!PREG || fwd_parent_in_regs<LV>(), "a register parent is the base or this group's previous body");
     auto& A = S.x.aba;
     const int b = fwd_sel<LV>(g, [](int x) { return x; });
     const int p = fwd_sel<LV>(g, [](int x) { return body_parent[x]; });
@@ -1164,7 +1194,11 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
     const T vmax = (T)P.max_coord_vel;
     T ap[6], r[3], ab[6], vs[6];
 #pragma unroll
-    for (int e = 0; e < 6; e++) { ap[e] = A.V[p][e] + in.c[e]; ab[e] = ap[e]; vs[e] = S.Vs[p][e]; }
+    for (int e = 0; e < 6; e++) {
+        ap[e] = (PREG ? pa[e] : A.V[p][e]) + in.c[e];
+        ab[e] = ap[e];
+        vs[e] = PREG ? pv[e] : S.Vs[p][e];
+    }
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         T t = in.uu[j];
@@ -1190,7 +1224,7 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
         for (int e = 0; e < 6; e++) vs[e] += in.Sc[i][e] * qn;
     }
 #pragma unroll
-    for (int e = 0; e < 6; e++) { A.V[b][e] = ab[e]; S.Vs[b][e] = vs[e]; }
+    for (int e = 0; e < 6; e++) { A.V[b][e] = ab[e]; S.Vs[b][e] = vs[e]; oa[e] = ab[e]; ov[e] = vs[e]; }
 }
 
 // ------------------------------------------------------------------------- one cooperative substep
@@ -1361,17 +1395,16 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     auto& A = S.x.aba;
     {
         AbaIn<T> in0, in1;
+        T kIA[21], kpa[6];   // the contribution to the parent of the body this group updated last
         aba_load<T, 0>(S, l >> 2, in0);
         aba_load<T, 1>(S, l >> 2, in1);
-        group_aba_level<T, 0>(P, S, l >> 2, dt, in0);
-        wave_sync();
+        group_aba_level<T, 0>(P, S, l >> 2, dt, in0, kIA, kpa, kIA, kpa);
         aba_load<T, 2>(S, l >> 2, in0);
-        group_aba_level<T, 1>(P, S, l >> 2, dt, in1);
-        wave_sync();
+        group_aba_level<T, 1>(P, S, l >> 2, dt, in1, kIA, kpa, kIA, kpa);
+        wave_sync();   // level 2 (the pelvis) reads both thighs' contributions from LDS
         aba_load<T, 3>(S, l >> 2, in1);
-        group_aba_level<T, 2>(P, S, l >> 2, dt, in0);
-        wave_sync();
-        group_aba_level<T, 3>(P, S, l >> 2, dt, in1);
+        group_aba_level<T, 2>(P, S, l >> 2, dt, in0, kIA, kpa, kIA, kpa);
+        group_aba_level<T, 3>(P, S, l >> 2, dt, in1, kIA, kpa, kIA, kpa);
     }
     __syncthreads();
     PHASE(3);
@@ -1405,18 +1438,16 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #pragma unroll
             for (int e = 0; e < 6; e++) { A.V[0][e] = a0[e]; S.Vs[0][e] = nus[e]; }
         }
-        wave_sync();
         SUBPHASE(15);
+        T fa[6], fv[6];   // acceleration and velocity of the body this group solved last
         fwd_load<T, 1>(S, l >> 2, fin1);
-        group_fwd_level<T, 0>(P, S, l >> 2, dt, fin0);
-        wave_sync();
+        group_fwd_level<T, 0>(P, S, l >> 2, dt, fin0, a0, nus, fa, fv);
         fwd_load<T, 2>(S, l >> 2, fin0);
-        group_fwd_level<T, 1>(P, S, l >> 2, dt, fin1);
-        wave_sync();
+        group_fwd_level<T, 1>(P, S, l >> 2, dt, fin1, fa, fv, fa, fv);
+        wave_sync();   // level 2 (thighs) reads the pelvis from LDS
         fwd_load<T, 3>(S, l >> 2, fin1);
-        group_fwd_level<T, 2>(P, S, l >> 2, dt, fin0);
-        wave_sync();
-        group_fwd_level<T, 3>(P, S, l >> 2, dt, fin1);
+        group_fwd_level<T, 2>(P, S, l >> 2, dt, fin0, fa, fv, fa, fv);
+        group_fwd_level<T, 3>(P, S, l >> 2, dt, fin1, fa, fv, fa, fv);
         if (l == 0) {
 #pragma unroll
             for (int q = 0; q < 21; q++) S.L0[q] = L[q];
