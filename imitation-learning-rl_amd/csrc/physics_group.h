@@ -1008,12 +1008,13 @@ __device__ __attribute__((always_inline)) void aba_load(const GroupLDS<T>& S, co
 }
 
 // Levels 1 and 3 take their first (level 3: only) child's contribution from registers: that child is the body the same
-// lane group updated one level earlier (kIA / kpa, the previous call's oIA / opa); levels 0 and 2 need not store theirs.
+// lane group updated one level earlier (kIA / kpa, the previous call's oIA / opa); only level 1 stores its result (the
+// pelvis and the base read the thighs and upper arms from LDS; the base reads lwaist from registers).
 template <typename T, int LV>
 __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams& P, GroupLDS<T>& S, const int g, const T dt,
                                                                const AbaIn<T>& in, const T* kIA, const T* kpa, T* oIA,
                                                                T* opa) {
-    constexpr bool KREG = LV == 1 || LV == 3, STORE = LV == 1 || LV == 3;
+    constexpr bool KREG = LV == 1 || LV == 3, STORE = LV == 1;   // level 3 (lwaist): the base reads it from registers
     auto& A = S.x.aba;
     constexpr int KM = aba_km<LV>();
     const int b = lvl_sel<LV>(g, [](int x) { return x; });
@@ -1393,9 +1394,9 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     //      contributions, and overwrites its IA/pA slots with its contribution to the parent (no longer
     //      needed itself).  The base step below sums the torso with lwaist and both upper arms.
     auto& A = S.x.aba;
+    T kIA[21], kpa[6];   // the contribution to the parent of the body this group updated last (after level 3: lwaist)
     {
         AbaIn<T> in0, in1;
-        T kIA[21], kpa[6];   // the contribution to the parent of the body this group updated last
         aba_load<T, 0>(S, l >> 2, in0);
         aba_load<T, 1>(S, l >> 2, in1);
         group_aba_level<T, 0>(P, S, l >> 2, dt, in0, kIA, kpa, kIA, kpa);
@@ -1417,10 +1418,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         fwd_load<T, 0>(S, l >> 2, fin0);   // read while the base solve runs
         T L[21], a0[6], IA0[21], nub[6];
 #pragma unroll
-        for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q] + A.IA[1][q] + A.IA[7][q] + A.IA[9][q];   // torso + kids
+        for (int q = 0; q < 21; q++) IA0[q] = A.IA[0][q] + kIA[q] + A.IA[7][q] + A.IA[9][q];   // torso + kids
         chol6_inv(IA0, L);
 #pragma unroll
-        for (int e = 0; e < 6; e++) a0[e] = -(A.pA[0][e] + A.pA[1][e] + A.pA[7][e] + A.pA[9][e]);
+        for (int e = 0; e < 6; e++) a0[e] = -(A.pA[0][e] + kpa[e] + A.pA[7][e] + A.pA[9][e]);
         chol6_solve_inv(L, a0);
 #pragma unroll
         for (int e = 0; e < 6; e++) nub[e] = S.nu[e];
