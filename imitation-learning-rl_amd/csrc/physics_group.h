@@ -486,6 +486,10 @@ __device__ inline void wave_sync() {   // cross-lane LDS ordering inside one wav
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// phase boundary of the cooperative substep: a block is one wavefront (EPB_ envs x 16 lanes <= 64), so LDS ordering
+// inside the wave suffices (no s_barrier, no drain of the wave's outstanding LDS writes).  The boundaries after the
+// contacts and the rows keep __syncthreads: spilled contacts and rows cross lanes through global memory.
+__device__ inline void phase_sync() { wave_sync(); }
 
 __device__ inline float med3(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 __device__ inline double med3(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
@@ -1235,6 +1239,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                                                              T* gblock, const int l, unsigned& ef,
                                                              unsigned long long tkey,   // tkey: terrain 2
                                                              const bool frozen = false) {   // env takes no step
+    static_assert(EPB_ * GL <= 64, "a block is one wavefront (phase_sync)");
     GroupLDS<T>& S = shb[ge];
     const ModelTab<T>& M = tab_fresh<T>();
     const T dt = (T)P.dt;
@@ -1283,7 +1288,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             cross3(ob, u, S.Sc[d] + 3);
         }
     }
-    __syncthreads();
+    phase_sync();
     PHASE(1);
     // ---- ABA pass 1: lane b = body b
     if (l < NB) {
@@ -1385,7 +1390,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #pragma unroll
         for (int q = 0; q < 21; q++) S.x.aba.IA[b][q] = IA[q];
     }
-    __syncthreads();
+    phase_sync();
     PHASE(2);
     // ---- ABA pass 2 (leaves -> root) by tree level: 4 steps {shins, lower arms} -> {thighs, upper arms}
     //      -> pelvis -> lwaist instead of 10 sequential bodies.  In a step, lane group g (4 lanes) updates
@@ -1407,7 +1412,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         group_aba_level<T, 2>(P, S, l >> 2, dt, in0, kIA, kpa, kIA, kpa);
         group_aba_level<T, 3>(P, S, l >> 2, dt, in1, kIA, kpa, kIA, kpa);
     }
-    __syncthreads();
+    phase_sync();
     PHASE(3);
     // ---- base + pass 3 (redundant on every lane); lane 0 publishes L0 and nu* = clamp(nu + dt acc)
     {
@@ -1456,7 +1461,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (int e = 0; e < 6; e++) S.nu[e] = nus[e];
         }
     }
-    __syncthreads();
+    phase_sync();
     PHASE(4);
     // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
     auto& C = S.x.cr;
@@ -1504,7 +1509,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         if (hiv) C.rdesc[pos + (int)lowv] = d | (1 << 8);
         nl += __popcll(gm1) + __popcll(gm2);
     }
-    __syncthreads();
+    phase_sync();
     PHASE(5);
     // ---- contacts, compacted in candidate order (ground points, then geom pairs)
     const int maxc = P.max_contacts < MAXC_G ? P.max_contacts : MAXC_G;
@@ -1881,7 +1886,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (int i = 0; i < 4; i++) S.st[3 + i] = nq[i] * nn;
         }
     }
-    __syncthreads();
+    phase_sync();
     PHASE(9);
 }
 
