@@ -2,7 +2,7 @@
 //
 // MI355X mapping: a 64-lane wavefront = 4 envs x 16 lanes; each env's working set lives in LDS
 // (struct GroupLDS, ~10 KB fp32), so a CU holds 16 envs (4 blocks of one wave: one wave per SIMD, the CU's
-// 160 KB; the kernel holds 512 VGPRs and spills 30 of them, 84 B of scratch per lane, tests/test_cpu_isa.py).
+// 160 KB; the kernel holds 512 VGPRs and spills 26 of them, 76 B of scratch per lane, tests/test_cpu_isa.py).
 // Same algorithm and operation order as physics.h (the per-lane kernel,
 // kept as the reference-shaped variant) except for the order of floating-point sums inside the
 // element-parallel ABA backward pass and the 16-lane DPP reductions of the PGS row products.
