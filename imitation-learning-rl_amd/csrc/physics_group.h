@@ -1725,9 +1725,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         };
         auto load_ln = [&](int ln_off) -> T { return *reinterpret_cast<const T*>(lds0 + ln_off); };
         const int neff = pool_rows(nl, nc);
-        // the zero rows of the pool layout (positions reserved by group_rows)
-        for (int z = nl + nc; z < neff; z++) {
-            if (pool_zero(z, nl, nc)) {
+        // the zero rows of the pool layout (positions reserved by group_rows): the gap after the normals and the
+        // trailing rows up to the minimum cycle length (pool_zero), visited directly rather than by scanning the frictions
+        {
+            auto zero_row = [&](int z) {
                 T* Z = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(pbase + z));
                 int n3, n3ln;
                 pgs_link<T>(pbase, z, nl, nc, n3, n3ln);
@@ -1735,7 +1736,10 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 if (l < RW - 2 - 3 * GL) Z[3 * GL + l] = T(0);
                 if (l == 0) *reinterpret_cast<int*>(Z + RO_S1 + 2) = n3;
                 if (l == 1) *reinterpret_cast<int*>(Z + RO_S1 + 3) = n3ln;
-            }
+            };
+            const int g0 = nl + nc, g1 = g0 + pool_gap(nc), u = pool_used(nl, nc);   // u >= g1
+            for (int z = g0; z < g1; z++) zero_row(z);
+            for (int z = u; z < neff; z++) zero_row(z);
         }
         wave_sync();
         const int total = P.iters * neff;
