@@ -749,7 +749,7 @@ __device__ inline bool pool_zero(int q, int nl, int nc) {   // position q holds 
 template <typename T>
 __device__ inline void pgs_link(int epos, int q, int nl, int nc, int& next3, int& next3_ln) {
     const int neff = pool_rows(nl, nc), f0 = nl + nc + pool_gap(nc);
-    const int t = (q + PGS_AHEAD) % neff;
+    const int t = q + PGS_AHEAD < neff ? q + PGS_AHEAD : q + PGS_AHEAD - neff;   // (q + PGS_AHEAD) % neff: q < neff, PGS_AHEAD < neff
     const bool fric = t >= f0 && t < pool_used(nl, nc);
     next3 = pool_off<T>(epos + t);
     next3_ln = pool_off<T>(epos + (fric ? nl + ((t - f0) >> 1) : t)) + RO_LAM * (int)sizeof(T);
