@@ -267,6 +267,88 @@ __device__ inline void small_inverse(const T* D, T* Di) {  // symmetric k x k (k
     }
 }
 
+// LDL^T factorisation of the symmetric positive definite k x k joint-space block D = S^T IA S (+ dt damping), k = K3,
+// stored 3x3: unit lower L (strict part in Lf), the reciprocal pivots idd, and D^-1 = L^-T diag(idd) L^-1 in Di.
+// Pass 2 downdates the articulated inertia through L and idd (Y = U L^-T; IA - sum_j Y_j Y_j^T idd_j: a sequence of
+// symmetric rank-1 terms, the dof-by-dof elimination of a chain of single-dof links) instead of W U^T with the
+// cofactor inverse: the cofactor determinant of a hip block cancels, and over 2048 lanes from identical states its
+// fp32 error ratio was p99 3.1 against 2.1 here (tools/fp32lab).
+template <typename T, int K3>
+__device__ inline void ldl_small(const T* D, T* Lf, T* idd, T* Di) {
+    T d[3];
+#pragma unroll
+    for (int j = 0; j < K3; j++) {
+        T s = D[4 * j];
+#pragma unroll
+        for (int q = 0; q < j; q++) s -= Lf[3 * j + q] * Lf[3 * j + q] * d[q];
+        d[j] = s;
+        idd[j] = prcp(s);
+#pragma unroll
+        for (int i = j + 1; i < K3; i++) {
+            T t = D[3 * i + j];
+#pragma unroll
+            for (int q = 0; q < j; q++) t -= Lf[3 * i + q] * Lf[3 * j + q] * d[q];
+            Lf[3 * i + j] = t * idd[j];
+        }
+    }
+    // M = L^-1 (unit lower), Di = M^T diag(idd) M
+    T Mi[9];
+#pragma unroll
+    for (int c = 0; c < K3; c++)
+#pragma unroll
+        for (int i = c; i < K3; i++) {
+            T t = i == c ? T(1) : T(0);
+#pragma unroll
+            for (int q = c; q < i; q++) t -= Lf[3 * i + q] * Mi[3 * q + c];
+            Mi[3 * i + c] = t;
+        }
+#pragma unroll
+    for (int i = 0; i < K3; i++)
+#pragma unroll
+        for (int j = i; j < K3; j++) {
+            T t = 0;
+#pragma unroll
+            for (int q = j; q < K3; q++) t += Mi[3 * q + i] * idd[q] * Mi[3 * q + j];
+            Di[3 * i + j] = t;
+            Di[3 * j + i] = t;
+        }
+}
+
+// pivot shifts (axes stay world-aligned): a spatial force about o_b moved to o_b - r (n += r x f); a spatial inertia
+// about o_b moved to o_b - r, I' = X^T I X with X = [[E, 0], [-[r]x, E]]:  B' = B + [r]x C, A' = A + [r]x B^T - B' [r]x
+template <typename T>
+__device__ inline void shift_force(const T* r, T* f) {
+    T x[3];
+    cross3(r, f + 3, x);
+    f[0] += x[0]; f[1] += x[1]; f[2] += x[2];
+}
+template <typename T>
+__device__ inline void shift_inertia(const T* r, T* I) {   // in place, sym6 packed (sidx)
+    T B[3][3], Bp[3][3], rb[3][3], rbp[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) B[i][j] = I[sidx(i, 3 + j)];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const T cj[3] = {I[sidx(3, 3 + j)], I[sidx(4, 3 + j)], I[sidx(5, 3 + j)]};
+        T x[3];
+        cross3(r, cj, x);
+#pragma unroll
+        for (int i = 0; i < 3; i++) Bp[i][j] = B[i][j] + x[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) { cross3(r, B[j], rb[j]); cross3(r, Bp[j], rbp[j]); }
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = i; j < 3; j++) I[sidx(i, j)] = I[sidx(i, j)] + rb[j][i] + rbp[i][j];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) I[sidx(i, 3 + j)] = Bp[i][j];
+}
+
 template <typename T>
 __device__ inline void chol6(const T* A, T* L) {  // A sym6 packed (sidx) -> L lower packed row-wise
     // L index for (i, j), j <= i: i*(i+1)/2 + j
@@ -340,43 +422,85 @@ __device__ inline void rotate_inertia(const T* R, const double* Il, T* Iw) {
 
 // Unconstrained accelerations: acc[NV] = [w_dot, v_com_dot (classical, world), qdd]
 // nu = [w(3), v_com(3), qd(17)];  tau = motor torques (dof order).
+//
+// Passes 1 and 2 run about each body's own pivot o_b (axes world-aligned): a body's spatial inertia carries its own
+// m |c - o_b|^2 (~0.01-0.1 m^2) instead of m |c|^2 about the common origin (up to ~1.4 m^2 for a foot), and its hinge
+// columns are [u; 0].  At the common origin the joint-space blocks S^T IA S were differences of m |c|^2-sized numbers,
+// which cost fp32 kernel steps 2-3x the rounding error of the fp32 oracle (tools/fp32lab).  A
+// child's articulated inertia and bias force are moved to its parent's pivot (shift_inertia / shift_force) before
+// they are summed there.  The torso's pivot is the common origin, so the base solve is unchanged, and pass 3, the
+// factorisation the constraint responses read (U, Dinv, L0) and c stay at the common origin.
 template <typename T>
 __device__ inline void aba(const PhysParams& P, const Kin<T>& K, const T* nu, const T* tau, Aba<T>& A, T* acc) {
-    T V[NB][6], IA[NB][21], pA[NB][6];
-    // ---- pass 1: velocities, bias accelerations, inertias, bias forces
+    T V[NB][6], IA[NB][21], pA[NB][6], cl[NB][6];
+    // ---- pass 1: velocities, bias accelerations, inertias, bias forces (about each pivot)
 #pragma unroll
     for (int b = 0; b < NB; b++) {
         if (b == 0) {
 #pragma unroll
-            for (int i = 0; i < 6; i++) { V[0][i] = nu[i]; A.c[0][i] = 0; }
+            for (int i = 0; i < 6; i++) { V[0][i] = nu[i]; A.c[0][i] = 0; cl[0][i] = 0; }
         } else {
             const int p = body_parent[b];
 #pragma unroll
-            for (int i = 0; i < 6; i++) { V[b][i] = V[p][i]; A.c[b][i] = 0; }
+            for (int i = 0; i < 6; i++) V[b][i] = V[p][i];
 #pragma unroll
             for (int k = 0; k < body_ndof[b]; k++) {
                 const int d = body_dof0[b] + k;
-                T S[6], Sq[6], cr[6];
+                T S[6];
                 motion_col(K, b, d, S);
                 const T qd = nu[6 + d];
 #pragma unroll
-                for (int i = 0; i < 6; i++) { Sq[i] = S[i] * qd; V[b][i] += Sq[i]; }
-                crm(V[b], Sq, cr);   // V^(k) x (S_k qd_k)
-#pragma unroll
-                for (int i = 0; i < 6; i++) A.c[b][i] += cr[i];
+                for (int i = 0; i < 6; i++) V[b][i] += S[i] * qd;
             }
         }
-        // inertia of the (merged) body at the origin
+    }
+    T Vl[NB][6];   // body velocities about their pivots: v_b = v_O + w x o_b
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        T x[3];
+        cross3(V[b], K.o[b], x);
+#pragma unroll
+        for (int i = 0; i < 3; i++) { Vl[b][i] = V[b][i]; Vl[b][3 + i] = V[b][3 + i] + x[i]; }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        if (b > 0) {
+            const int p = body_parent[b];
+            // bias acceleration about the pivot: sum_k V^(k) x [u_k qd_k; 0], V^(0) the parent's velocity moved to o_b
+            T Vk[6], x[3];
+            cross3(V[p], K.o[b], x);
+#pragma unroll
+            for (int i = 0; i < 3; i++) { Vk[i] = V[p][i]; Vk[3 + i] = V[p][3 + i] + x[i]; cl[b][i] = 0; cl[b][3 + i] = 0; }
+#pragma unroll
+            for (int k = 0; k < body_ndof[b]; k++) {
+                const int d = body_dof0[b] + k;
+                const T qd = nu[6 + d];
+                const T uq[3] = {K.u[d][0] * qd, K.u[d][1] * qd, K.u[d][2] * qd};
+#pragma unroll
+                for (int i = 0; i < 3; i++) Vk[i] += uq[i];
+                T wx[3], vx[3];
+                cross3(Vk, uq, wx);
+                cross3(Vk + 3, uq, vx);
+#pragma unroll
+                for (int i = 0; i < 3; i++) { cl[b][i] += wx[i]; cl[b][3 + i] += vx[i]; }
+            }
+            // the same at the common origin (pass 3): v_O = v_b - w x o_b
+            T y[3];
+            cross3(cl[b], K.o[b], y);
+#pragma unroll
+            for (int i = 0; i < 3; i++) { A.c[b][i] = cl[b][i]; A.c[b][3 + i] = cl[b][3 + i] - y[i]; }
+        }
+        // inertia of the (merged) body about its pivot
         T Icw[9], c[3];
 #pragma unroll
         for (int i = 0; i < 3; i++)
-            c[i] = K.o[b][i] + K.R[b][3 * i] * (T)body_com[3 * b] + K.R[b][3 * i + 1] * (T)body_com[3 * b + 1] +
+            c[i] = K.R[b][3 * i] * (T)body_com[3 * b] + K.R[b][3 * i + 1] * (T)body_com[3 * b + 1] +
                    K.R[b][3 * i + 2] * (T)body_com[3 * b + 2];
         rotate_inertia(K.R[b], body_inertia + 9 * b, Icw);
         spatial_inertia((T)body_mass[b], c, Icw, IA[b]);
         T h[6];
-        symmv(IA[b], V[b], h);
-        crf(V[b], h, pA[b]);
+        symmv(IA[b], Vl[b], h);
+        crf(Vl[b], h, pA[b]);
         // gravity on the body COM
         const T mg = -(T)body_mass[b] * (T)P.gravity;
         pA[b][0] -= c[1] * mg;   // (c x F)_x with F = (0,0,mg)
@@ -387,103 +511,115 @@ __device__ inline void aba(const PhysParams& P, const Kin<T>& K, const T* nu, co
 #pragma unroll
     for (int l = 0; l < NLINK; l++) {
         const int b = link_body[l];
-        T cl[3], vc[3], Iw[9], wI[3];
+        T cp[3], vc[3], Iw[9], wI[3];
 #pragma unroll
         for (int i = 0; i < 3; i++)
-            cl[i] = K.o[b][i] + K.R[b][3 * i] * (T)link_com[3 * l] + K.R[b][3 * i + 1] * (T)link_com[3 * l + 1] +
+            cp[i] = K.R[b][3 * i] * (T)link_com[3 * l] + K.R[b][3 * i + 1] * (T)link_com[3 * l + 1] +
                     K.R[b][3 * i + 2] * (T)link_com[3 * l + 2];
-        cross3(V[b], cl, vc);
+        cross3(Vl[b], cp, vc);
 #pragma unroll
-        for (int i = 0; i < 3; i++) vc[i] += V[b][3 + i];
+        for (int i = 0; i < 3; i++) vc[i] += Vl[b][3 + i];
         const T kv = (T)P.lin_damp * (T(1) + sqrt(dot3(vc, vc)));
-        const T kw = (T)P.ang_damp * (T(1) + sqrt(dot3(V[b], V[b])));
+        const T kw = (T)P.ang_damp * (T(1) + sqrt(dot3(Vl[b], Vl[b])));
         rotate_inertia(K.R[b], link_inertia + 9 * l, Iw);
 #pragma unroll
-        for (int i = 0; i < 3; i++) wI[i] = Iw[3 * i] * V[b][0] + Iw[3 * i + 1] * V[b][1] + Iw[3 * i + 2] * V[b][2];
+        for (int i = 0; i < 3; i++) wI[i] = Iw[3 * i] * Vl[b][0] + Iw[3 * i + 1] * Vl[b][1] + Iw[3 * i + 2] * Vl[b][2];
         const T m = (T)link_mass[l];
         T F[3], n[3], cxF[3];
 #pragma unroll
         for (int i = 0; i < 3; i++) { F[i] = -m * vc[i] * kv; n[i] = -wI[i] * kw; }
-        cross3(cl, F, cxF);
+        cross3(cp, F, cxF);
 #pragma unroll
         for (int i = 0; i < 3; i++) { pA[b][i] -= n[i] + cxF[i]; pA[b][3 + i] -= F[i]; }
     }
-    // ---- pass 2: articulated inertias (leaves -> root), no coordinate transforms
+    // ---- pass 2: articulated inertias (leaves -> root), about each pivot; hinge columns [u; 0]
 #pragma unroll
     for (int b = NB - 1; b >= 1; b--) {
         const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];
-        T S[3][6], D[9], Di[9];
+        T Ul[3][6], D[9], Di[9], Lf[9], idd[3];
 #pragma unroll
         for (int j = 0; j < k; j++) {
-            motion_col(K, b, d0 + j, S[j]);
-            symmv(IA[b], S[j], A.U[d0 + j]);
+            const T* u = K.u[d0 + j];
+#pragma unroll
+            for (int e = 0; e < 6; e++) Ul[j][e] = IA[b][sidx(e, 0)] * u[0] + IA[b][sidx(e, 1)] * u[1] + IA[b][sidx(e, 2)] * u[2];
         }
 #pragma unroll
         for (int i = 0; i < k; i++)
 #pragma unroll
-            for (int j = 0; j < k; j++) {
-                T s = 0;
-#pragma unroll
-                for (int e = 0; e < 6; e++) s += S[i][e] * A.U[d0 + j][e];
-                D[3 * i + j] = s;
-            }
+            for (int j = 0; j < k; j++) D[3 * i + j] = dot3(K.u[d0 + i], Ul[j]);
 #pragma unroll
         for (int j = 0; j < k; j++) {
-            T sp = 0;
-#pragma unroll
-            for (int e = 0; e < 6; e++) sp += S[j][e] * pA[b][e];
-            T uj = tau[d0 + j] - sp;
+            T uj = tau[d0 + j] - dot3(K.u[d0 + j], pA[b]);
             if (P.joint_damping) {
                 D[4 * j] += (T)P.dt * (T)dof_damping[d0 + j];
                 uj -= (T)dof_damping[d0 + j] * nu[6 + d0 + j];
             }
             A.uu[d0 + j] = uj;
         }
-        if (k == 1) small_inverse<T, 1>(D, Di);
-        else if (k == 2) small_inverse<T, 2>(D, Di);
-        else small_inverse<T, 3>(D, Di);
+        if (k == 1) ldl_small<T, 1>(D, Lf, idd, Di);
+        else if (k == 2) ldl_small<T, 2>(D, Lf, idd, Di);
+        else ldl_small<T, 3>(D, Lf, idd, Di);
 #pragma unroll
         for (int i = 0; i < 9; i++) A.Dinv[b][i] = Di[i];
-        // W = U Dinv  (6 x k)
-        T W[3][6];
+        // W = U Dinv (6 x k), Y = U L^-T
+        T W[3][6], Y[3][6];
 #pragma unroll
         for (int j = 0; j < k; j++)
 #pragma unroll
             for (int e = 0; e < 6; e++) {
-                T s = 0;
+                T s = 0, y = Ul[j][e];
 #pragma unroll
-                for (int i = 0; i < k; i++) s += A.U[d0 + i][e] * Di[3 * i + j];
+                for (int i = 0; i < k; i++) s += Ul[i][e] * Di[3 * i + j];
+#pragma unroll
+                for (int q = 0; q < j; q++) y -= Lf[3 * j + q] * Y[q][e];
                 W[j][e] = s;
+                Y[j][e] = y;
             }
-        // Ia = IA - W U^T ; pa = pA + Ia c + W u
+        // Ia = IA - sum_j Y_j Y_j^T idd_j ; pa = pA + Ia c + W u
 #pragma unroll
         for (int r = 0; r < 6; r++)
 #pragma unroll
             for (int cc = r; cc < 6; cc++) {
-                T s = 0;
+                T s = IA[b][sidx(r, cc)];
 #pragma unroll
-                for (int j = 0; j < k; j++) s += W[j][r] * A.U[d0 + j][cc];
-                IA[b][sidx(r, cc)] -= s;
+                for (int j = 0; j < k; j++) s -= Y[j][r] * idd[j] * Y[j][cc];
+                IA[b][sidx(r, cc)] = s;
             }
-        T Iac[6];
-        symmv(IA[b], A.c[b], Iac);
+        T Iac[6], pa[6];
+        symmv(IA[b], cl[b], Iac);
 #pragma unroll
         for (int e = 0; e < 6; e++) {
             T s = pA[b][e] + Iac[e];
 #pragma unroll
             for (int j = 0; j < k; j++) s += W[j][e] * A.uu[d0 + j];
-            pA[p][e] += s;
+            pa[e] = s;
         }
+        // to the parent's pivot: r = o_b - o_p
+        T r[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) r[i] = K.o[b][i] - K.o[p][i];
+        shift_force(r, pa);
+        shift_inertia(r, IA[b]);
+#pragma unroll
+        for (int e = 0; e < 6; e++) pA[p][e] += pa[e];
 #pragma unroll
         for (int i = 0; i < 21; i++) IA[p][i] += IA[b][i];
+        // U at the common origin for pass 3 and the constraint responses: [U_n + o_b x U_f; U_f]
+#pragma unroll
+        for (int j = 0; j < k; j++) {
+            T x[3];
+            cross3(K.o[b], Ul[j] + 3, x);
+#pragma unroll
+            for (int i = 0; i < 3; i++) { A.U[d0 + j][i] = Ul[j][i] + x[i]; A.U[d0 + j][3 + i] = Ul[j][3 + i]; }
+        }
     }
-    // ---- base
+    // ---- base (the torso's pivot is the common origin)
     chol6(IA[0], A.L0);
     T a[NB][6];
 #pragma unroll
     for (int i = 0; i < 6; i++) a[0][i] = -pA[0][i];
     chol6_solve(A.L0, a[0]);
-    // ---- pass 3: accelerations
+    // ---- pass 3: accelerations (common origin)
 #pragma unroll
     for (int b = 1; b < NB; b++) {
         const int p = body_parent[b], k = body_ndof[b], d0 = body_dof0[b];

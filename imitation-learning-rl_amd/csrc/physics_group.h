@@ -367,7 +367,8 @@ struct GroupLDS {   // ~9.7 KB (fp32): 4 blocks of 4 envs per CU = one wavefront
     union {
         struct {   // articulated-body pass (dead once the accelerations are known)
             // IA rows padded to 24 words: 16-byte aligned, so a row moves in six 16-byte LDS accesses
-            T V[NB][6], c[NB][6];
+            // c: bias accelerations at the common origin (pass 3), cl: about each body's pivot (pass 2)
+            T V[NB][6], c[NB][6], cl[NB][6];
             alignas(16) T IA[NB][24];
             T pA[NB][6], uu[NDOF + 1];   // V: pass-3 body accelerations
         } aba;
@@ -984,7 +985,7 @@ __device__ __attribute__((always_inline)) inline T lvl_damp(int g, int j) {
 // The inputs of a level's body that pass 1 (or the FK) wrote: loaded one level early, while the previous level
 // computes, so the LDS latency of only the children's contributions stays on the level-to-level chain.
 template <typename T>
-struct AbaIn { T IA[21], pA[6], c[6], Sc[3][6], tau[3], qd[3]; };
+struct AbaIn { T IA[21], pA[6], c[6], u[3][3], tau[3], qd[3], ob[3], op[3]; };
 template <int LV>
 constexpr int aba_km() {   // the level's largest dof count (1, 3, 1, 2): smaller bodies of the level are padded to it
     int m = 0;
@@ -1001,11 +1002,15 @@ __device__ __attribute__((always_inline)) void aba_load(const GroupLDS<T>& S, co
 #pragma unroll
     for (int q = 0; q < 21; q++) in.IA[q] = A.IA[b][q];
 #pragma unroll
-    for (int e = 0; e < 6; e++) { in.pA[e] = A.pA[b][e]; in.c[e] = A.c[b][e]; }
+    for (int e = 0; e < 6; e++) { in.pA[e] = A.pA[b][e]; in.c[e] = A.cl[b][e]; }
+    const int p = lvl_sel<LV>(g, [](int x) { return body_parent[x]; });
+#pragma unroll
+    for (int i = 0; i < 3; i++) { in.ob[i] = S.o[b][i]; in.op[i] = S.o[p][i]; }
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         const int d = j < k ? d0 + j : d0;
-        load_sc(S, d, in.Sc[j]);
+#pragma unroll
+        for (int i = 0; i < 3; i++) in.u[j][i] = S.Sc[d][i];
         in.tau[j] = S.tau[d];
         in.qd[j] = S.nu[6 + d];
     }
@@ -1024,7 +1029,7 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
     const int b = lvl_sel<LV>(g, [](int x) { return x; });
     const int k = lvl_sel<LV>(g, [](int x) { return body_ndof[x]; });
     const int d0 = lvl_sel<LV>(g, [](int x) { return body_dof0[x]; });
-    T IA[21], pAb[6], cb[6], Sc[3][6], U[3][6], D[9], Di[9], uj[3], W[3][6];
+    T IA[21], pAb[6], cb[6], u[3][3], U[3][6], D[9], Di[9], uj[3], W[3][6];
 #pragma unroll
     for (int q = 0; q < 21; q++) IA[q] = in.IA[q];
 #pragma unroll
@@ -1048,52 +1053,49 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
         add_kid(g == 0 ? LVL_KID[LV][0][0] : (g == 1 ? LVL_KID[LV][1][0] : (g == 2 ? LVL_KID[LV][2][0] : LVL_KID[LV][3][0])));
     if constexpr (LVL_KID[LV][0][1] >= 0)
         add_kid(g == 0 ? LVL_KID[LV][0][1] : (g == 1 ? LVL_KID[LV][1][1] : (g == 2 ? LVL_KID[LV][2][1] : LVL_KID[LV][3][1])));
+    // about the body's pivot its hinge columns are [u; 0]: U = IA[:, 0:3] u, D = u . U[0:3], S^T pA = u . pA[0:3]
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         const bool on = j < k;
 #pragma unroll
-        for (int e = 0; e < 6; e++) Sc[j][e] = on ? in.Sc[j][e] : T(0);
-        symmv(IA, Sc[j], U[j]);
-        T sp = 0;
+        for (int i = 0; i < 3; i++) u[j][i] = on ? in.u[j][i] : T(0);
 #pragma unroll
-        for (int e = 0; e < 6; e++) sp += Sc[j][e] * pAb[e];
-        T t = in.tau[j] - sp;
+        for (int e = 0; e < 6; e++) U[j][e] = IA[sidx(e, 0)] * u[j][0] + IA[sidx(e, 1)] * u[j][1] + IA[sidx(e, 2)] * u[j][2];
+        T t = in.tau[j] - dot3(u[j], pAb);
         if (P.joint_damping) t -= lvl_damp<LV, T>(g, j) * in.qd[j];
         uj[j] = on ? t : T(0);
     }
 #pragma unroll
     for (int i = 0; i < KM; i++) {
 #pragma unroll
-        for (int j = 0; j < KM; j++) {
-            T t = 0;
-#pragma unroll
-            for (int e = 0; e < 6; e++) t += Sc[i][e] * U[j][e];
-            D[3 * i + j] = t;
-        }
+        for (int j = 0; j < KM; j++) D[3 * i + j] = dot3(u[i], U[j]);
         const bool on = i < k;
         if (P.joint_damping) D[4 * i] += dt * lvl_damp<LV, T>(g, i);
         D[4 * i] = on ? D[4 * i] : T(1);   // identity pivot for padded dofs
     }
-#pragma unroll
-    for (int q = 0; q < 9; q++) Di[q] = q % 4 == 0 ? T(1) : T(0);   // identity outside the KM block
-    small_inverse<T, KM>(D, Di);
+    // LDL^T of the block (physics.h::ldl_small); the downdate through Y = U L^-T, W = U Dinv for the bias force
+    T Lf[9], idd[3], Y[3][6];
+    ldl_small<T, KM>(D, Lf, idd, Di);
 #pragma unroll
     for (int j = 0; j < KM; j++)
 #pragma unroll
         for (int e = 0; e < 6; e++) {
-            T t = 0;
+            T t = 0, y = U[j][e];
 #pragma unroll
             for (int i = 0; i < KM; i++) t += U[i][e] * Di[3 * i + j];
+#pragma unroll
+            for (int q = 0; q < j; q++) y -= Lf[3 * j + q] * Y[q][e];
             W[j][e] = t;
+            Y[j][e] = y;
         }
-    // Ia = IA - W U^T (in place), pa = pA + Ia c + W u
+    // Ia = IA - sum_j Y_j idd_j Y_j^T (in place), pa = pA + Ia c + W u
 #pragma unroll
     for (int r = 0; r < 6; r++)
 #pragma unroll
         for (int cc = r; cc < 6; cc++) {
             T t = IA[sidx(r, cc)];
 #pragma unroll
-            for (int j = 0; j < KM; j++) t -= W[j][r] * U[j][cc];
+            for (int j = 0; j < KM; j++) t -= Y[j][r] * idd[j] * Y[j][cc];
             IA[sidx(r, cc)] = t;
         }
     T pa[6];
@@ -1104,6 +1106,13 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 #pragma unroll
         for (int j = 0; j < KM; j++) t += W[j][e] * uj[j];
         pa[e] = t;
+    }
+    {   // to the parent's pivot
+        T r[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) r[i] = in.ob[i] - in.op[i];
+        shift_force(r, pa);
+        shift_inertia(r, IA);
     }
     // contribution to the parent in the body's own (now dead) slots; factorisation for passes 3 / responses.
     // The 4 lanes of a group (and groups sharing a body) write identical values.
@@ -1120,8 +1129,10 @@ __device__ __attribute__((always_inline)) void group_aba_level(const PhysParams&
 #pragma unroll
     for (int j = 0; j < KM; j++) {
         if (j < k) {
+            T x[3];   // U at the common origin (pass 3, the constraint responses): [U_n + o_b x U_f; U_f]
+            cross3(in.ob, U[j] + 3, x);
 #pragma unroll
-            for (int e = 0; e < 6; e++) S.U[d0 + j][e] = U[j][e];
+            for (int e = 0; e < 3; e++) { S.U[d0 + j][e] = U[j][e] + x[e]; S.U[d0 + j][3 + e] = U[j][3 + e]; }
             A.uu[d0 + j] = uj[j];
         }
     }
@@ -1312,27 +1323,36 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             }
         }
         SUBPHASE(13);
-        T cb[6] = {0, 0, 0, 0, 0, 0};
-        const int k = body_ndof_l(b), d0 = body_dof0_l(b);
-        for (int j = 0; j < k; j++) {
-            const int d = d0 + j;
-            T Sq[6], cr[6];
-            load_sc(S, d, Sq);
-            const T qd = S.nu[6 + d];
-#pragma unroll
-            for (int e = 0; e < 6; e++) { Sq[e] *= qd; V[e] += Sq[e]; }
-            crm(V, Sq, cr);
-#pragma unroll
-            for (int e = 0; e < 6; e++) cb[e] += cr[e];
-        }
+        // passes 1 and 2 run about the body's own pivot o_b (physics.h::aba): the parent's velocity moved to o_b,
+        // then the body's dofs, whose columns there are [u; 0]; bias acceleration sum_k V^(k) x [u_k qd_k; 0]
         T Rb[9], ob[3];
 #pragma unroll
         for (int i = 0; i < 9; i++) Rb[i] = S.R[b][i];
 #pragma unroll
         for (int i = 0; i < 3; i++) ob[i] = S.o[b][i];
+        {
+            T x[3];
+            cross3(V, ob, x);
+#pragma unroll
+            for (int i = 0; i < 3; i++) V[3 + i] += x[i];
+        }
+        T cb[6] = {0, 0, 0, 0, 0, 0};
+        const int k = body_ndof_l(b), d0 = body_dof0_l(b);
+        for (int j = 0; j < k; j++) {
+            const int d = d0 + j;
+            const T qd = S.nu[6 + d];
+            const T uq[3] = {S.Sc[d][0] * qd, S.Sc[d][1] * qd, S.Sc[d][2] * qd};
+#pragma unroll
+            for (int i = 0; i < 3; i++) V[i] += uq[i];
+            T wx[3], vx[3];
+            cross3(V, uq, wx);
+            cross3(V + 3, uq, vx);
+#pragma unroll
+            for (int i = 0; i < 3; i++) { cb[i] += wx[i]; cb[3 + i] += vx[i]; }
+        }
         T c3[3], Icw[9], IA[21], h[6], pA[6];
 #pragma unroll
-        for (int i = 0; i < 3; i++) c3[i] = ob[i] + Rb[3 * i] * M.com[b][0] + Rb[3 * i + 1] * M.com[b][1] + Rb[3 * i + 2] * M.com[b][2];
+        for (int i = 0; i < 3; i++) c3[i] = Rb[3 * i] * M.com[b][0] + Rb[3 * i + 1] * M.com[b][1] + Rb[3 * i + 2] * M.com[b][2];
         {
             T RI[9];
 #pragma unroll
@@ -1357,7 +1377,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             const int lk = body_link0_l(b) + q;
             T cl[3], vc[3], Iw[9], wI[3];
 #pragma unroll
-            for (int i = 0; i < 3; i++) cl[i] = ob[i] + Rb[3 * i] * M.lcom[lk][0] + Rb[3 * i + 1] * M.lcom[lk][1] + Rb[3 * i + 2] * M.lcom[lk][2];
+            for (int i = 0; i < 3; i++) cl[i] = Rb[3 * i] * M.lcom[lk][0] + Rb[3 * i + 1] * M.lcom[lk][1] + Rb[3 * i + 2] * M.lcom[lk][2];
             cross3(V, cl, vc);
 #pragma unroll
             for (int i = 0; i < 3; i++) vc[i] += V[3 + i];
@@ -1385,8 +1405,14 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #pragma unroll
             for (int i = 0; i < 3; i++) { pA[i] -= n[i] + cxF[i]; pA[3 + i] -= F[i]; }
         }
+        T cx[3];   // the bias acceleration at the common origin for pass 3: v_O = v_b - w x o_b
+        cross3(cb, ob, cx);
 #pragma unroll
-        for (int e = 0; e < 6; e++) { S.x.aba.c[b][e] = cb[e]; S.x.aba.pA[b][e] = pA[e]; }
+        for (int e = 0; e < 6; e++) {
+            S.x.aba.cl[b][e] = cb[e];
+            S.x.aba.c[b][e] = e < 3 ? cb[e] : cb[e] - cx[e - 3];
+            S.x.aba.pA[b][e] = pA[e];
+        }
 #pragma unroll
         for (int q = 0; q < 21; q++) S.x.aba.IA[b][q] = IA[q];
     }

@@ -13,7 +13,7 @@
 Tolerances: frame, timestep and the RNG counter bit-exact everywhere.  fp64 kernel: state 1e-6 after a full
 step (different but exact formulations), obs 1e-5, reward 1e-5, done exact.  fp32 kernel
 (the benchmarked build) vs the fp64 oracle over ONE step from the identical state, held to the error of the
-oracle's own physics run in float arithmetic from that state (the fp32 yardstick): see FP32_FLOOR / FP32_RATIO
+oracle's own physics run in float arithmetic from that state (the fp32 yardstick): see FP32_LANE_QUANTILES
 and SENS_BOUND below.  A k = 32 variant steps the benchmark's launch shape (hum_step_k, 4096 lanes).
 """
 import json
@@ -39,26 +39,28 @@ from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 # one fp32 env step vs the fp64 oracle from the same state ("fp32 step bound").  The yardstick
 # is the oracle's own physics instantiated in float arithmetic (oracle/physics_oracle_f32.c) stepped from the same
 # state: its distance from the fp64 oracle is the rounding error intrinsic to an fp32 step of this algorithm
-# (measured: 3e-5 - 8e-5 in the joint speeds, above SURVEY's 1e-5 - no fp32 step of this physics meets 1e-5).  The
-# envelope is that error's max over FP32_REALISATIONS fp32-oracle steps per lane: from the lane's state and from the
-# state perturbed by 2^-24 relative (one float32 rounding of the input, which an fp32 step cannot resolve).  On the
-# well-conditioned lanes the kernel must stay, per obs block (the 8 body terms, the 17 joint positions, the 17 joint
-# speeds) and for the reward, within max(FP32_FLOOR, FP32_RATIO x the envelope's max), and its median over the lanes
-# within FP32_P50_RATIO x the unperturbed fp32 oracle's median (the max of a few dozen heavy-tailed draws is noisy, the
-# median is not); the 28 clip-table values differ only by their float32 output rounding (<= FP32_FLOOR).  Over ALL lanes
-# (ill-conditioned ones included) the reward stays within max(1e-4, 2 x the envelope's).
+# (measured: up to 2.5e-4 in the joint speeds, above SURVEY's 1e-5 - no fp32 step of this physics meets 1e-5).  The
+# lane's envelope is that error's max over FP32_REALISATIONS fp32-oracle steps: from the lane's state and from the
+# state perturbed by 2^-24 relative (one float32 rounding of the input, which an fp32 step cannot resolve).
+#
+# The gate is PER LANE (round 5): on every well-conditioned lane and obs block (the 8 body terms, the 17 joint
+# positions, the 17 joint speeds) the ratio kernel error / the same lane's envelope is formed, and over FP32_LANES
+# lanes its quantiles must stay within FP32_LANE_QUANTILES - the kernel's typical error no larger than the yardstick's
+# and its tail (p90, p99) within 1.5x and 3x of it.  Targets stated before the measurement, met by
+# the pivot-local ABA (physics.h::aba); the round-4 world-frame ABA measured p90 2.75 / p99 7.8 on joint speeds and
+# fails it.  The per-lane error is heavy-tailed (a lane on the edge of a limit or contact switch: max ratios 4 - 12
+# for every build) so the maximum is bounded absolutely instead (FP32_ABS_MAX: twice the largest fp32-oracle
+# envelope measured over 2048 lanes, tools/fp32lab).  The 28 clip-table values differ only by their float32 output
+# rounding (<= FP32_FLOOR).  Over ALL lanes (ill-conditioned ones included) the reward stays within max(1e-4, 2 x the
+# envelope's).
 FP32_FLOOR = {"obs": 1e-5, "reward": 1e-5}
 FP32_RATIO = 1.5
 FP32_REALISATIONS = 4
-# lanes the fp32 maxima are taken over.  The per-lane error is heavy-tailed (kernel / same-lane envelope: median
-# 0.5 - 0.9, max 2.5 - 12 over 512 lanes, identical for every build measured, profiles/r04_fp32ab.txt): over 64 lanes
-# the max is one lane's draw, and a build whose rollout happens to sample one tail lane more fails the max-vs-max
-# ratio with an unchanged error distribution (observed).  Over 256 lanes both maxima estimate the same high quantile.
-FP32_LANES = 256
-# the kernel's typical (median) joint-speed error is measured at 1.7 - 2.1x the fp32 oracle's (its world-frame spatial
-# algebra against the oracle's local frames; the hardware rcp / rsqrt approximations account for ~10 %: the
-# HUM_EXACT_MATH variant measured 1.7 - 2.1x as well, profiles/r04_fp32_accuracy.txt), its maximum within the envelope
-FP32_P50_RATIO = 3.0
+FP32_LANES = 512
+FP32_LANE_QUANTILES = {50: 1.0, 90: 1.5, 99: 3.0}
+# ratio denominators below this are raised to it: errors under ~1 float32 ulp of an O(1) observation are not compared
+FP32_LANE_FLOOR = 1e-7
+FP32_ABS_MAX = {"body": 1e-4, "joint_pos": 1e-4, "joint_vel": 6e-4}
 # the fixed bound the short-scenario tests (the hier golden scenarios, terrain) still use: 2x round 2's worst
 # measured conditioned error
 FP32_BOUND = {"obs_max": 1e-4, "reward_max": 1e-5}
@@ -173,6 +175,11 @@ def rollout_and_compare(clips, precision, n=4096, steps=200, per_clip=64, seed=2
     return flags, {k: (np.array(v) if isinstance(v, list) else v) for k, v in st.items()}
 
 
+def _quantiles(r):
+    return {"p50": float(np.median(r)), "p90": float(np.percentile(r, 90)), "p99": float(np.percentile(r, 99)),
+            "max": float(r.max()), "lanes": int(len(r))}
+
+
 def _summary(tag, st):
     good = st["sens"] <= SENS_BOUND
     s = {"lanes": st["lanes"], "obs_max": float(st["obs"].max()), "obs_p99": float(np.percentile(st["obs"], 99)),
@@ -203,7 +210,9 @@ def _summary(tag, st):
                            "fp32_oracle_rms": rms(ov[:, ix].max(1)), "kernel_p50": float(np.median(kv[:, ix].max(1))),
                            "fp32_oracle_p50": float(np.median(ov[:, ix].max(1))),
                            "lanes_kernel": [float(x) for x in kv[:, ix].max(1)],
-                           "lanes_fp32_oracle": [float(x) for x in ov[:, ix].max(1)]}
+                           "lanes_fp32_oracle": [float(x) for x in ov[:, ix].max(1)],
+                           "lanes_fp32_envelope": [float(x) for x in ev[:, ix].max(1)],
+                           "lane_ratio": _quantiles(kv[:, ix].max(1) / np.maximum(ev[:, ix].max(1), FP32_LANE_FLOOR))}
                        for b, ix in OBS_BLOCKS.items()},
             "per_component": {"kernel": [float(x) for x in kv.max(0)], "fp32_oracle": [float(x) for x in ov.max(0)],
                               "fp32_envelope": [float(x) for x in ev.max(0)]}}
@@ -243,8 +252,10 @@ def _check_fp32(s):
             if b == "clip_table":   # float32 output rounding of the float64 table values only
                 assert v["kernel"] <= FP32_FLOOR["obs"], (b, v)
                 continue
-            assert v["kernel"] <= max(FP32_FLOOR["obs"], FP32_RATIO * v["fp32_envelope"]), (b, v)
-            assert v["kernel_p50"] <= max(1e-7, FP32_P50_RATIO * v["fp32_oracle_p50"]), (b, v)
+            q = v["lane_ratio"]
+            for pct, bound in FP32_LANE_QUANTILES.items():
+                assert q["p%d" % pct] <= bound, (b, "p%d" % pct, q)
+            assert v["kernel"] <= FP32_ABS_MAX[b], (b, v["kernel"])
         env = o32["envelope"]
         assert s["reward_max_conditioned"] <= max(FP32_FLOOR["reward"], FP32_RATIO * env["reward_max_conditioned"])
         assert s["reward_max"] <= max(1e-4, 2 * env["reward_max"]), (s["reward_max"], env)
@@ -294,6 +305,8 @@ def _agents_of(robs):
 
 
 def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23):
+    """per_kind lanes of each transition kind; the fp32 test takes FP32_LANES // 2 of each (the high-level ones take
+    no physics step: their low-level obs errors are 0)"""
     from ilrl_amd.hier_env import HierVecEnv, HIER_CLIP
     clip = load_clip(HIER_CLIP)
     env = HierVecEnv(n, seed=seed, precision=precision)
@@ -390,7 +403,7 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
 def test_hier_full_size_rollout_sample_matches_oracle(precision):
     """Config 5 at full size: 4096 lanes, 200 auto-reset transitions, then 64 high-level and 64 low-level
     transitions vs the oracle from the injected lane state (hier_env.py:355-366, 538-642)."""
-    flags, st = hier_rollout_and_compare(precision)
+    flags, st = hier_rollout_and_compare(precision, per_kind=FP32_LANES // 2 if precision == "fp32" else 64)
     assert flags & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
     assert st["exact_ok"], "agents / frame / timestep / RNG counter / level counters differ from the oracle"
     s = _summary("c5_%s" % precision, st)

@@ -7,7 +7,7 @@ default library) produces the states; every library in LIBS then steps exactly t
 per library, ILRL_AMD_LIB), and all are compared with the fp64 oracle and the fp32 oracle yardstick on the same
 N lanes (the test's per-block statistics: max, p99, p90, p50).
 
-usage: LIBS="base new" [N=512] [STEPS=192] python3 tools/diag_fp32_ab.py   (on a GPU box; writes gpurun_out/fp32ab/)
+usage: LIBS="base new new@0" [N=512] [STEPS=192] python3 tools/diag_fp32_ab.py   (on a GPU box; writes gpurun_out/fp32ab/)
 """
 import json
 import os
@@ -26,7 +26,8 @@ N_ENV = 4096
 BLOCKS = {"body": np.arange(0, 8), "joint_pos": np.arange(8, 42, 2), "joint_vel": np.arange(9, 42, 2)}
 
 
-def lib_path(v):
+def lib_path(v):   # "name" or "name@K": the library libhumenv_<name>.so ("new": libhumenv.so), kernel K (default 1)
+    v = v.split("@")[0]
     return os.path.join(LIBDIR, "libhumenv.so" if v == "new" else "libhumenv_%s.so" % v)
 
 
@@ -48,7 +49,8 @@ def step_states(tag):
     import torch
     from ilrl_amd.vec_env import HumanoidVecEnv
     z = np.load(os.path.join(OUT, "states.npz"))
-    env = HumanoidVecEnv(N_ENV, clips=("motion02_04",), seed=21, precision="fp32")
+    kernel = int(tag.split("@")[1]) if "@" in tag else 1   # 0: the per-lane kernel (physics.h)
+    env = HumanoidVecEnv(N_ENV, clips=("motion02_04",), seed=21, precision="fp32", kernel=kernel)
     env.set_state(z["phys"], z["book"])
     obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(z["a"], device="cuda"))]
     env.close()
