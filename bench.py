@@ -7,8 +7,9 @@ step), auto-reset of done lanes inside the launch.  A "step" = one env step of e
 observation + imitation reward + bookkeeping); `--k K` env steps run per hum_step_k launch (outputs written
 per step, [K, n, ...]), and every rate below is per env-step.  Multi-GPU: one process per GPU, lanes sharded
 by rank (global lane ids -> identical per-lane streams regardless of N), no data-path collective -> weak
-scaling; `--gather-every G` adds the trajectory gather (ONE all-gather of the last G steps' obs / action /
-reward / done rows every G env steps, the only collective the path has), timed separately.
+scaling; the trajectory gather (`--gather-every G`, default k when WORLD_SIZE > 1: the last G steps' obs / action /
+reward / done rows of every rank gathered to rank 0 every G env steps, the only collective the path has)
+runs asynchronously beside the next launches and is completed inside the timed region.
 
 Prints ONE JSON line on rank 0.  Every number in it is measured in this run except `roofline.traffic`
 (PMC bytes, profiles/pmc_traffic.json, from a rocprofv3 --pmc pass of this same command) and the static FLOP
@@ -49,8 +50,9 @@ def parse():
     ap.add_argument("--phys", action="append", default=[], help="physics override k=v (hum_config field), diagnostics")
     ap.add_argument("--hier", action="store_true",
                     help="config 5: HierarchicalHumanoidEnv two-level rollout (hum_hier_step), clip motion09_03")
-    ap.add_argument("--gather-every", type=int, default=0,
-                    help="multi-GPU: trajectory all-gather of the last G env steps every G env steps (G %% k == 0)")
+    ap.add_argument("--gather-every", type=int, default=None,
+                    help="trajectory gather to rank 0 of the last G env steps every G env steps (G %% k == 0); default "
+                         "k when WORLD_SIZE > 1 (the learner's trajectory feed, SURVEY 8(e)), 0 = none")
     ap.add_argument("--k", type=int, default=K_DEFAULT, help="env steps per launch (hum_step_k)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise torch.distributed and run every collective (barriers, the timing all-reduce, the "
@@ -207,10 +209,10 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     sizes, wsizes = launch_sizes(steps, k), launch_sizes(warmup, k)
     launches, wlaunches = len(sizes), len(wsizes)
     pool, hpool = _pools(a, dev, n, k, rank)
-    G = a.gather_every
-    if G and (G % k or steps % k):
-        raise SystemExit("--gather-every: it and --steps must be multiples of --k")
-    ring = [None] * (G // k if G else 1)   # output buffers of the launches since the last gather
+    G = a.gather_every if a.dist and not a.policy else 0
+    if G and G % k:
+        raise SystemExit("--gather-every must be a multiple of --k")
+    ring = [None]   # the launch's output buffers (packed into the gather fragment right after the launch)
     rem_out = {}   # output buffers of the shorter remainder launches, by size
     if a.hier:
         from ilrl_amd.hier_env import HierVecEnv
@@ -260,7 +262,18 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     env.done.zero_()
     for w in range(wlaunches):
         step(w, wsizes[w])
-    gather_s, gathered = 0.0, []
+    gather_s, gathered, tg = 0.0, [], None
+    gdiag = os.environ.get("ILRL_GATHER_DIAG", "")   # diagnostics: "pack" = packing only, "comm" = the gather only
+    if G:   # the trajectory gather: static shapes, packed lane-major fragments, asynchronous (parallel.TrajectoryGather)
+        from ilrl_amd.parallel import TrajectoryGather, shard
+        o = ring[0] if ring[0] is not None else env.step_k_out(k)
+        ring[0] = o
+        cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])   # obs (hier: low-level), reward, done
+        fields = [("obs", tuple(cols[0].shape[2:]), cols[0].dtype), ("act", (17,), pool[0].dtype),
+                  ("reward", tuple(cols[1].shape[2:]), cols[1].dtype), ("done", tuple(cols[2].shape[2:]), cols[2].dtype)]
+        tg = TrajectoryGather(fields, [shard(n * world, world, r)[1] for r in range(world)], G, dev)
+        tg.start(0)   # communicator setup (RCCL point-to-point pairs) outside the timed region
+        tg.wait()
     if not a.policy:
         # every output buffer the timed launches write exists before the clock starts (a warmup shorter than k, e.g.
         # the driver's --steps 20 --warmup 5, never ran a launch of the timed shape: its allocation and zero fill
@@ -281,14 +294,28 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     ev0.record(stream)
     for s in range(launches):
         step(s, sizes[s])
-        if G and a.dist and not a.policy and ((s + 1) * k) % G == 0:
-            tg = time.perf_counter()
-            frag = _fragment(a, ring, [pool[(s - j) % 16] for j in range(len(ring) - 1, -1, -1)])
-            from ilrl_amd.parallel import gather_trajectories
-            got = gather_trajectories(frag, dst=0)
-            if got is not None and a.dump_gather:
-                gathered.append([x[::a.dump_lane_stride].cpu() for x in got])
-            gather_s += time.perf_counter() - tg
+        if tg is not None:
+            th = time.perf_counter()
+            slot = (s * k // G) % 2
+            o = ring[0]
+            cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])
+            kk = sizes[s]
+            act = pool[s % 16][:kk]
+            if kk < k:   # the remainder launch's outputs
+                o = rem_out[kk]
+                cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])
+            if gdiag != "comm":
+                tg.pack(slot, (s * k) % G, {"obs": cols[0], "act": act, "reward": cols[1], "done": cols[2]})
+            if gdiag != "pack" and ((s * k + kk) % G == 0 or s == launches - 1):   # a full fragment, or the last one
+                tg.start(slot)
+                if a.dump_gather:   # tests: rank 0 keeps the fragment (synchronous)
+                    tg.wait(slot)
+                    got = tg.result(slot)
+                    if got is not None:
+                        gathered.append([got[f][::a.dump_lane_stride].cpu() for f in ("obs", "act", "reward", "done")])
+            gather_s += time.perf_counter() - th
+    if tg is not None:
+        tg.wait()   # the last fragments' gathers complete inside the timed region
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if a.dist:
@@ -315,16 +342,6 @@ def _all_reduce(world, dev, backend, x, op):
     t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=op)
     return float(t.item())
-
-
-def _fragment(a, ring, acts):
-    """The last G env steps as lane-major buffers [n, G, ...] for the gather: obs, action, reward, done (hier: the
-    low-level obs / action / reward and done of every transition)."""
-    import torch
-    cat = lambda xs: torch.cat(xs, dim=0).transpose(0, 1).contiguous()
-    if a.hier:
-        return [cat([r[2] for r in ring]), cat(acts), cat([r[4] for r in ring]), cat([r[5] for r in ring])]
-    return [cat([r[0] for r in ring]), cat(acts), cat([r[1] for r in ring]), cat([r[2] for r in ring])]
 
 
 def count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank):
@@ -362,6 +379,13 @@ def main():
     # one process per GPU; ranks beyond the visible devices share them (tests on a one-GPU box)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     if a.dist:
+        if "RANK" not in os.environ:   # --force-dist outside torch.distributed.run: a one-rank group of its own
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(sk.getsockname()[1]))
+            sk.close()
         torch.cuda.set_device(dev)
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -379,6 +403,8 @@ def main():
         a.k = 1   # closed loop: the policy acts on every step's observation, one launch each
     if a.k < 1:
         raise SystemExit("--k must be >= 1")
+    if a.gather_every is None:
+        a.gather_every = a.k if world > 1 and not a.policy else 0
     env, wall_max, kern_ms, low_steps, gather_s, gathered, sizes = run(a, world, rank, dev, n, a.precision, a.steps,
                                                                        a.warmup, phys)
     flags = env.error_flags()
@@ -434,9 +460,12 @@ def main():
             out["unit"] = "env-steps/s"
             out["physics_env_steps_per_step"] = phys_steps_per_step
             out["agent_transitions_per_s"] = total / wall_max
-        if a.dist and a.gather_every:
-            out["gather"] = {"every": a.gather_every, "seconds": gather_s, "backend": a.backend,
-                             "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1), "fragments": len(gathered) or None}
+        if a.dist and a.gather_every and not a.policy:
+            out["gather"] = {"every": a.gather_every, "backend": a.backend, "to_rank": 0,
+                             "op": "dist.gather of one packed lane-major fragment (RCCL point-to-point), asynchronous, "
+                                   "double-buffered; completed inside the timed region",
+                             "host_seconds": gather_s, "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1),
+                             "fragments": -(-a.steps // a.gather_every)}
         if world == 1 and not a.no_secondary and not a.hier and not a.policy:
             from ilrl_amd.clips import CLIP_NAMES
             clips = tuple(CLIP_NAMES) if a.clip == "all" else (a.clip,)

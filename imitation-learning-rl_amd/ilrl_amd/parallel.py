@@ -7,6 +7,8 @@
   call over torch.distributed ("nccl" = RCCL over xGMI on MI355X, "gloo" on CPU).  The buffers travel as their
   raw bytes (lossless for every dtype), and uneven shards are padded to the largest one and trimmed on arrival.
 """
+import math
+
 import torch
 import torch.distributed as dist
 
@@ -23,13 +25,14 @@ def _row_bytes(t):
     return t[0].numel() * t.element_size() if t.dim() > 1 else t.element_size()
 
 
-def gather_trajectories(tensors, dst=0):
+def gather_trajectories(tensors, dst=0, counts=None):
     """Gather per-rank trajectory buffers (same trailing shape and dtype on every rank; leading dim = that
     rank's lanes, may differ between ranks) onto `dst` as one [sum n_r, ...] tensor each, in rank order.
 
     All buffers are packed, row by row, into ONE uint8 message (their raw bytes: int64 / uint8 / float keep
     their exact values), so RCCL moves one large payload per call: xGMI is point-to-point, so few large
-    collectives beat many small ones.  Returns the list on dst, None elsewhere."""
+    collectives beat many small ones.  `counts` (every rank's lane count, e.g. from `shard`) skips the count
+    exchange.  Returns the list on dst, None elsewhere.  (The benchmark's repeated gather is TrajectoryGather.)"""
     on = dist.is_initialized()   # one rank with the group initialised still runs the collectives (bench --force-dist)
     world = dist.get_world_size() if on else 1
     rank = dist.get_rank() if on else 0
@@ -45,10 +48,11 @@ def gather_trajectories(tensors, dst=0):
     if not on:
         full, counts = flat, [n]
     else:
-        cnt = torch.tensor([n], dtype=torch.int64, device=dev)
-        counts_t = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(counts_t, cnt)
-        counts = [int(c.item()) for c in counts_t]
+        if counts is None:
+            cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+            counts_t = [torch.zeros_like(cnt) for _ in range(world)]
+            dist.all_gather(counts_t, cnt)
+            counts = [int(c.item()) for c in counts_t]
         m = max(counts)
         pad = torch.zeros((m, flat.shape[1]), dtype=torch.uint8, device=dev)
         pad[:n] = flat
@@ -70,3 +74,106 @@ def gather_trajectories(tensors, dst=0):
         out.append(col.view(t.dtype).reshape((full.shape[0],) + tuple(t.shape[1:])))
         c += w
     return out
+
+
+class TrajectoryGather:
+    """The rollout's repeated trajectory gather to the learner rank (reference: RLlib's rollout workers
+    ship sample batches to the learner, /root/reference/train_config.py:33-34), built once per run.
+
+    * Static shapes: every rank's lane count is known from the sharding (`counts`, e.g. `shard`), so no count
+      exchange and no host synchronisation happen per call.
+    * One packed, lane-major uint8 buffer per fragment: lane i's row holds its G steps of every field (raw bytes,
+      fields ordered by descending item size so each typed view is aligned).  `pack` writes a launch's
+      time-major outputs [k, n, ...] into the fragment's typed views - one strided device copy per field, the only
+      copy - and the whole fragment travels as ONE message.
+    * Asynchronous: `start` issues the gather (RCCL point-to-point sends to `dst`, `dist.gather`) ordered after the
+      packs on the current stream and returns; the next env launches proceed while it moves.  Fragments alternate
+      between `slots` buffers; packing into a slot first makes the stream wait for that slot's previous gather.
+    * gloo (CPU tests): the same layout, gathered synchronously through host memory.
+    """
+
+    def __init__(self, fields, counts, G, device, dst=0, slots=2):
+        self.on = dist.is_initialized()
+        self.world = dist.get_world_size() if self.on else 1
+        self.rank = dist.get_rank() if self.on else 0
+        if len(counts) != self.world:
+            raise ValueError("counts: one lane count per rank")
+        self.counts, self.G, self.dst, self.dev = [int(c) for c in counts], int(G), dst, torch.device(device)
+        self.n, self.m = self.counts[self.rank], max(self.counts)
+        self.nccl = self.on and dist.get_backend() == "nccl"
+        self.fields = []   # (name, per-step trailing shape, dtype, byte offset in the row, bytes per step)
+        off = 0
+        for name, shape, dtype in sorted(fields, key=lambda f: -torch.empty(0, dtype=f[2]).element_size()):
+            isz = torch.empty(0, dtype=dtype).element_size()
+            w = int(math.prod(shape)) * isz
+            self.fields.append((name, tuple(shape), dtype, off, w))
+            off += self.G * w
+        self.order = [f[0] for f in fields]
+        self.W = -(-off // 8) * 8   # row width: a multiple of the largest item size
+        self.send = [torch.zeros((self.m, self.W), dtype=torch.uint8, device=self.dev) for _ in range(slots)]
+        self.recv = [[torch.empty((self.m, self.W), dtype=torch.uint8, device=self.dev if self.nccl else "cpu")
+                      for _ in range(self.world)] if self.rank == dst else None for _ in range(slots)]
+        self.work = [None] * slots
+        self.fragments = 0
+
+    def _view(self, buf, name, rows=None):
+        for nm, shape, dtype, off, w in self.fields:
+            if nm == name:
+                b = buf[:rows] if rows is not None else buf
+                return b[:, off:off + self.G * w].view(dtype).view((b.shape[0], self.G) + shape)
+        raise KeyError(name)
+
+    def pack(self, slot, t0, outputs):
+        """outputs: {field: [k, n, ...] time-major tensor of steps t0 .. t0 + k - 1 of the fragment}.  On the device
+        one hum_pack_rows launch copies every field (the HIP library's packing kernel); on the host, torch copies."""
+        if self.work[slot] is not None:   # the slot's previous gather must have read the buffer
+            self.work[slot].wait()
+            self.work[slot] = None
+        if self.dev.type == "cuda":
+            return self._pack_native(slot, t0, outputs)
+        for name, x in outputs.items():
+            self._view(self.send[slot], name, self.n)[:, t0:t0 + x.shape[0]].copy_(x.transpose(0, 1))
+
+    def _pack_native(self, slot, t0, outputs):
+        import ctypes
+        from . import _native as N
+        kk = None
+        arr = (N.HumPackField * len(outputs))()
+        base = self.send[slot].data_ptr()
+        for j, (name, x) in enumerate(outputs.items()):
+            nm, shape, dtype, off, w = next(f for f in self.fields if f[0] == name)
+            if x.dtype != dtype or tuple(x.shape[2:]) != shape or x.shape[1] != self.n or x.stride(-1) != 1 and w > x.element_size():
+                raise ValueError("pack: field %s has shape %s / dtype %s" % (name, tuple(x.shape), x.dtype))
+            if kk is None:
+                kk = int(x.shape[0])
+            isz = x.element_size()
+            arr[j].src, arr[j].dst = x.data_ptr(), base + off
+            arr[j].src_step, arr[j].src_lane = x.stride(0) * isz, x.stride(1) * isz
+            arr[j].dst_step, arr[j].dst_lane, arr[j].row_bytes = w, self.W, w
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        N.check(N.lib().hum_pack_rows(arr, len(outputs), kk, self.n, t0, ctypes.c_void_p(stream)), "hum_pack_rows")
+
+    def start(self, slot):
+        """Gather slot's packed fragment onto dst (asynchronous on RCCL)."""
+        self.fragments += 1
+        if not self.on:
+            if self.recv[slot] is not None:
+                self.recv[slot][0].copy_(self.send[slot])
+            return
+        if self.nccl:
+            self.work[slot] = dist.gather(self.send[slot], gather_list=self.recv[slot], dst=self.dst, async_op=True)
+        else:   # gloo gathers host tensors
+            dist.gather(self.send[slot].cpu(), gather_list=self.recv[slot], dst=self.dst)
+
+    def wait(self, slot=None):
+        for j in range(len(self.work)) if slot is None else [slot]:
+            if self.work[j] is not None:
+                self.work[j].wait()
+                self.work[j] = None
+
+    def result(self, slot):
+        """dst: the gathered fragment as {field: [sum n_r, G, ...]} in rank order (after wait); None elsewhere."""
+        if self.recv[slot] is None:
+            return None
+        full = torch.cat([r[:c] for r, c in zip(self.recv[slot], self.counts)], dim=0)
+        return {nm: self._view(full, nm) for nm in self.order}

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 10
+#define HUM_ABI_VERSION 11
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -292,6 +292,21 @@ int hum_hier_step(hum_env* env, const float* high_act, const float* low_act, con
 int hum_hier_step_k(hum_env* env, const float* high_act, const float* low_act, const uint8_t* agent, uint8_t* agents,
                     float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done, int32_t* frame,
                     uint32_t flags, float* high_obs_reset, int32_t k, void* stream);
+
+/* ---- Trajectory packing for the learner feed (reference: RLlib rollout workers ship SampleBatches of
+ * obs / actions / rewards / dones to the learner, train_config.py:33-34).  One launch copies k steps x n lanes of up to
+ * HUM_PACK_MAX_FIELDS row fields from their time-major step outputs (row (t, i) at src + t * src_step + i * src_lane
+ * bytes, e.g. hum_step_k's [k,n,70] obs) into a lane-major record buffer (row (t, i) at dst + i * dst_lane +
+ * (t0 + t) * dst_step bytes): each lane's record then holds its steps contiguously, and a rank's whole fragment is one
+ * message for the gather.  Rows are copied as raw bytes (row_bytes a multiple of 4, or 1 for u8 fields of width 1). */
+#define HUM_PACK_MAX_FIELDS 6
+typedef struct {
+    const void* src;
+    void* dst;
+    int64_t src_step, src_lane, dst_step, dst_lane;   /* byte strides */
+    int32_t row_bytes;
+} hum_pack_field;
+int hum_pack_rows(const hum_pack_field* fields, int32_t nfields, int32_t k, int32_t n, int32_t t0, void* stream);
 
 /* ---- On-GPU policy inference: the reference's PPO policy network (train_config.py:107-111,
  * RLlib FullyConnectedNetwork, fcnet_hiddens [256, 256], tanh, free_log_std) evaluated on the env's device

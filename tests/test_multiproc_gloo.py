@@ -75,3 +75,69 @@ def test_gloo_world2_gather_and_rng_independent_of_sharding(n_total):
     np.testing.assert_array_equal(f64, np.arange(n_total, dtype=np.float64) / 3.0)
     single = np.array([[O.lane_draw(5, i, c, 0, 293) for c in range(3)] for i in range(n_total)], dtype=np.float32)
     np.testing.assert_array_equal(draws, single)
+
+
+def _tg_worker(rank, world, port, n_total, q):
+    """TrajectoryGather (the benchmark's repeated gather): static counts, packed lane-major fragments, two slots,
+    launches of k = 4 steps into fragments of G = 8 steps, and a final partial fragment (3 steps)."""
+    from ilrl_amd.parallel import TrajectoryGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, n = shard(n_total, world, rank)
+    counts = [shard(n_total, world, r)[1] for r in range(world)]
+    G, k = 8, 4
+    fields = [("obs", (70,), torch.float32), ("act", (17,), torch.float32), ("reward", (), torch.float32),
+              ("done", (), torch.uint8), ("frame", (), torch.int64)]
+    tg = TrajectoryGather(fields, counts, G, "cpu")
+    got = []
+    sizes = [k, k, k, k, 3]   # 19 steps: fragments [0, 8), [8, 16), [16, 19)
+
+    def rows(t0, kk):   # time-major [kk, n, ...] values that name (global lane, step)
+        t = torch.arange(t0, t0 + kk, dtype=torch.float64).reshape(kk, 1)
+        lane = torch.arange(off, off + n, dtype=torch.float64).reshape(1, n)
+        v = lane * 1000 + t
+        return {"obs": (v.unsqueeze(-1) + torch.arange(70, dtype=torch.float64) / 100).float(),
+                "act": (v.unsqueeze(-1) - torch.arange(17, dtype=torch.float64)).float(),
+                "reward": v.float(), "done": ((lane + t) % 2 == 0).to(torch.uint8), "frame": (v * (1 << 33)).long()}
+    t = 0
+    for s, kk in enumerate(sizes):
+        slot = (t // G) % 2
+        tg.pack(slot, t % G, rows(t, kk))
+        t += kk
+        if t % G == 0 or s == len(sizes) - 1:
+            tg.start(slot)
+            tg.wait(slot)
+            r = tg.result(slot)
+            if r is not None:
+                got.append({f: x.clone().numpy() for f, x in r.items()})
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("n_total", [10, 7])
+def test_gloo_world2_trajectory_gather_fragments(n_total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tg_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == 3
+    lane = np.arange(n_total, dtype=np.float64).reshape(-1, 1)
+    for j, nsteps in enumerate((8, 8, 3)):
+        f = got[j]
+        assert f["obs"].shape == (n_total, 8, 70) and f["done"].dtype == np.uint8 and f["frame"].dtype == np.int64
+        t = np.arange(8 * j, 8 * j + nsteps, dtype=np.float64).reshape(1, -1)
+        v = lane * 1000 + t
+        np.testing.assert_array_equal(f["reward"][:, :nsteps], v.astype(np.float32))
+        np.testing.assert_array_equal(f["obs"][:, :nsteps], (v[..., None] + np.arange(70) / 100).astype(np.float32))
+        np.testing.assert_array_equal(f["act"][:, :nsteps], (v[..., None] - np.arange(17)).astype(np.float32))
+        np.testing.assert_array_equal(f["done"][:, :nsteps], ((lane + t) % 2 == 0).astype(np.uint8))
+        np.testing.assert_array_equal(f["frame"][:, :nsteps], (v * (1 << 33)).astype(np.int64))
