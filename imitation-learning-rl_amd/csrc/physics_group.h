@@ -528,7 +528,7 @@ __device__ inline void chol6_inv(const T* A, T* L) {
         T s = A[sidx(j, j)];
 #pragma unroll
         for (int k = 0; k < j; k++) s -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
-        const T inv = prsqrt(s);
+        const T inv = prsqrt_piv(s);
         L[j * (j + 1) / 2 + j] = inv;
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
@@ -845,7 +845,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
                 for (int i = 0; i < 3; i++) lat[i] = vr[i] - n[i] * vn;
                 const T l2 = dot3(lat, lat);
                 if (l2 > (T)1e-12) {
-                    const T il = prsqrt(l2);
+                    const T il = prsqrt_row(l2);
 #pragma unroll
                     for (int i = 0; i < 3; i++) t1[i] = lat[i] * il;
                     cross3(t1, n, t2);
@@ -874,7 +874,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];   // limit rows: sg * Mi[6 + d] (sg^2 = 1)
         sc[1] = 0;   // lo = 0 for every row type: the PGS reads this slot as its zero pad
         sc[3] = 0;
-        sc[4] = prcp(jm);
+        sc[4] = prcp_row(jm);
         const int p = epos + pool_pos(r, enl, enc);
         // coupling c_r = J_r . (M^-1 J^T)_pred(r) from the lane that solved the predecessor row in this round
         // (ds_bpermute); predecessors in another round are left to the LDS pass below
@@ -1668,7 +1668,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 d = dist - ra - rb;
                 hit = d < (T)P.contact_thresh && dist > (T)1e-9;
                 if (hit) {
-                    const T idist = prcp(dist);
+                    const T idist = prcp_geo(dist);
 #pragma unroll
                     for (int i = 0; i < 3; i++) {
                         n[i] = dv[i] * idist;

@@ -56,7 +56,10 @@ from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 FP32_FLOOR = {"obs": 1e-5, "reward": 1e-5}
 FP32_RATIO = 1.5
 FP32_REALISATIONS = 4
-FP32_LANES = 512
+FP32_LANES = 512   # per config; config 2 (the benchmarked workload, k = 1 and k = 32) twice as many
+# The floor of these ratios: another fp32 realisation of the oracle itself against the 4-realisation envelope measures
+# p50 0.72, p90 1.2, p99 1.9 - 2.3, max 3 - 4.4 on joint speeds (512 and 2048 lanes, the bench's states); the p99 over
+# 512 lanes (the 5th largest ratio) varies by +-0.5 between state samples for one build, hence 1024 lanes for config 2.
 FP32_LANE_QUANTILES = {50: 1.0, 90: 1.5, 99: 3.0}
 # ratio denominators below this are raised to it: errors under ~1 float32 ulp of an O(1) observation are not compared
 FP32_LANE_FLOOR = 1e-7
@@ -230,7 +233,7 @@ def test_full_size_rollout_no_drop_and_sample_matches_oracle(config, precision, 
     """k = 32: the benchmark's launch shape (4096 lanes, 32 env steps per hum_step_k launch)."""
     clips = ("motion02_04",) if config == "c2" else tuple(CLIP_NAMES)
     # fp32: the per-block maxima are compared over FP32_LANES lanes (per clip: 64 for the four-clip config 3)
-    per_clip = FP32_LANES // len(clips) if precision == "fp32" else 64
+    per_clip = FP32_LANES * (2 if config == "c2" else 1) // len(clips) if precision == "fp32" else 64
     flags, st = rollout_and_compare(clips, precision, steps=192 if k > 1 else 200, k=k, per_clip=per_clip)
     assert flags & N.HUM_EFLAG_CONTACT_OVERFLOW == 0, "a contact was dropped"
     assert flags & N.HUM_EFLAG_NONFINITE_ACTION == 0
