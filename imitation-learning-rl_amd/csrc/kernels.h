@@ -268,7 +268,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
 #pragma unroll
         for (int k = 0; k < NDOF; k++) js[k] = js_pre[k];
     }
-    SUBPHASE(19);
+    POST_SUBPHASE(19);
     b.robot_pos[0] = pp.bx; b.robot_pos[1] = pp.by; b.robot_pos[2] = 0;
     // updateReward (:441-465)
     double dJ = 0, dV = 0;
@@ -307,7 +307,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
     total = total + b.alive * REWARD_W[5];
     total = total + b.bps * REWARD_W[6];
     inc_frame(b, c, 2);                                                      // :513
-    SUBPHASE(20);
+    POST_SUBPHASE(20);
     // checkTarget (:412-434)
     {
         const double dist = norm3_blas(b.robot_pos[0] - b.target[0], b.robot_pos[1] - b.target[1], b.robot_pos[2] - b.target[2]);
@@ -323,7 +323,7 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         }
         set_walk_target_hl(b);
     }
-    SUBPHASE(21);
+    POST_SUBPHASE(21);
     ref_obs(c, b.frame, obs + 42, ef);                                        // :519
     bool done;                                                                // :521-524
     {
@@ -334,16 +334,16 @@ __device__ __attribute__((always_inline)) void post_step(const KArgs& a, int i, 
         b.timestep += 1;
         if (b.timestep >= 3000) done = true;
     }
-    SUBPHASE(22);
+    POST_SUBPHASE(22);
     float* orow = obs_dst ? obs_dst : a.obs + io * HUM_NOBS;
 #pragma unroll
     for (int k = 0; k < HUM_NOBS; k++)
         if (!js_pre || k < 8 || k >= 42) orow[k] = obs[k];
-    SUBPHASE(16);
+    POST_SUBPHASE(16);
     a.rew[io] = (float)total;
     a.done[io] = done ? 1 : 0;
     if (a.frame_out) a.frame_out[io] = b.frame;
-    SUBPHASE(23);
+    POST_SUBPHASE(23);
     if (defer_reset) {
         *defer_reset = done && (a.flags & HUM_STEP_AUTORESET);
         return;
@@ -974,7 +974,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         a.agents[io] = 0;
     } else if (valid && l == 0) {
         load_book(a, i, b, a.hier != 0);
-        SUBPHASE(17);
+        POST_SUBPHASE(17);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
             nonfinite_outputs(a, io, b.frame, a.hier ? nullptr : ostage);
@@ -995,7 +995,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             }
         }
     }
-    SUBPHASE(18);
+    POST_SUBPHASE(18);
     if (!a.hier) {
         // auto-reset (low-level env): lane 0 draws the start frame (reset_lane's first draw), the env's lanes
         // compute the reset pose's hinge sin / cos, lane 0 finishes reset_lane with them

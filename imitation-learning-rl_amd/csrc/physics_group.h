@@ -15,6 +15,8 @@
 //   rows            one constraint row per lane: Jacobian + test-impulse response M^-1 J^T
 //   PGS             rows in Bullet order; J.nu over the 16 lanes by DPP row_ror reductions
 #pragma once
+#include <utility>
+
 #include "physics.h"
 #include "terrain.h"
 
@@ -478,6 +480,14 @@ static __shared__ unsigned long long s_tlast;   // shared: markers also sit insi
 #else
 #define SUBPHASE(k) do { } while (0)
 #endif
+// HUM_SUBPHASE_PGS: the Delassus PGS's own split (markers 19-22) in place of the post-step ones
+#ifdef HUM_SUBPHASE_PGS
+#define PGS_SUBPHASE(k) SUBPHASE(k)
+#define POST_SUBPHASE(k) do { } while (0)
+#else
+#define PGS_SUBPHASE(k) do { } while (0)
+#define POST_SUBPHASE(k) SUBPHASE(k)
+#endif
 
 #ifdef HUM_CHECK_LINKS
 __device__ unsigned g_check[8];
@@ -756,24 +766,41 @@ __device__ inline void pgs_link(int epos, int q, int nl, int nc, int& next3, int
     next3_ln = pool_off<T>(epos + (fric ? nl + ((t - f0) >> 1) : t)) + RO_LAM * (int)sizeof(T);
 }
 
+// The Delassus-form PGS (pgs_delassus below; -DHUM_DELASSUS builds only: measured slower) runs
+// when every env of the wave has at most LMAX rows, the block's rows all sit in its LDS pool, and the wave is the
+// benchmarked fp32 one of 4 envs (one MFMA wave).
+constexpr int LMAX = NV;   // a row's J slots hold its Delassus row: LMAX <= NV
+#ifdef HUM_DELASSUS
+constexpr bool DELASSUS_ON = true;
+#else
+constexpr bool DELASSUS_ON = false;
+#endif
+template <typename T, int EPB_>
+constexpr bool delassus_kernel() { return DELASSUS_ON && sizeof(T) == 4 && EPB_ == 4; }
+
 template <typename T, int EPB_>
 __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, GroupLDS<T>* shb, T* gblock, int nl, int nc,
-                                                          const T dt, int& pbase, int& ptot) {
+                                                          const T dt, int& pbase, int& ptot, bool& lam) {
     const ModelTab<T>& M = tab_fresh<T>();
     const int lane = threadIdx.x & 63, cap = P.lds_rows;
     const T idt = T(1) / dt;
-    // pre: task prefix (actual rows); pos: pool prefix (short envs are padded with zero rows, see PGS)
+    // pre: task prefix (actual rows); pos: pool prefix (velocity form: short envs are padded with zero rows, see PGS;
+    // Delassus form: the rows back to back, no padding)
     int cnt[EPB_], nls[EPB_], ncs[EPB_], pre[EPB_ + 1], pos[EPB_ + 1];
     pre[0] = 0;
     pos[0] = 0;
+    int nmax = 0;
 #pragma unroll
     for (int e = 0; e < EPB_; e++) {
         nls[e] = __builtin_amdgcn_readlane(nl, e * GL);
         ncs[e] = __builtin_amdgcn_readlane(nc, e * GL);
         cnt[e] = nls[e] + 3 * ncs[e];
         pre[e + 1] = pre[e] + cnt[e];
-        pos[e + 1] = pos[e] + pool_rows(nls[e], ncs[e]);
+        nmax = max(nmax, cnt[e]);
     }
+    lam = delassus_kernel<T, EPB_>() && pre[EPB_] <= cap && nmax <= LMAX;   // the Delassus-form PGS (wave-uniform)
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) pos[e + 1] = pos[e] + (lam ? cnt[e] : pool_rows(nls[e], ncs[e]));
     pbase = 0;
 #pragma unroll
     for (int q = 0; q < EPB_; q++)
@@ -875,11 +902,16 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         sc[1] = 0;   // lo = 0 for every row type: the PGS reads this slot as its zero pad
         sc[3] = 0;
         sc[4] = prcp_row(jm);
-        const int p = epos + pool_pos(r, enl, enc);
+        const int p = epos + (lam ? r : pool_pos(r, enl, enc));
         // coupling c_r = J_r . (M^-1 J^T)_pred(r) from the lane that solved the predecessor row in this round
-        // (ds_bpermute); predecessors in another round are left to the LDS pass below
+        // (ds_bpermute); predecessors in another round are left to the LDS pass below.  The Delassus-form PGS stores
+        // instead the row's velocity J_r . nu* (the constraint velocity its residual starts from) and, in the link slot,
+        // the LDS offset of the lambda that bounds it (its normal row's for a friction row, its own otherwise)
         T qc = T(0);
-        {
+        if (lam) {
+#pragma unroll
+            for (int q = 0; q < NV; q++) qc += J[q] * S.nu[q];
+        } else {
             const int qr = p - epos, qp = qr == 0 ? pool_rows(enl, enc) - 1 : qr - 1;
             const int rp = qp < enl + enc ? qp : qp - pool_gap(enc);
             const int tp = (t - r) + rp, t0 = t - lane;
@@ -903,7 +935,12 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         }
         if (p < cap) {
             int n3, n3ln;
-            pgs_link<T>(epos, p - epos, enl, enc, n3, n3ln);   // (used only when all of the block's rows are in LDS)
+            if (lam) {   // dense layout: the normal row of friction row r is row enl + (r - enl - enc) / 2
+                n3 = 0;
+                n3ln = pool_off<T>(r >= enl + enc ? epos + enl + ((r - enl - enc) >> 1) : p) + RO_LAM * (int)sizeof(T);
+            } else {
+                pgs_link<T>(epos, p - epos, enl, enc, n3, n3ln);   // (used only when all of the block's rows are in LDS)
+            }
             store_row(reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(p)), J, Mi, sc, n3, n3ln, qc);
         }
         else {
@@ -913,7 +950,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
     // couplings c_r = J_r . (M^-1 J^T)_pred(r) (cyclic predecessor; 0 after a zero row) for the lookahead
     // PGS, which needs them only when the block's rows all sit in LDS: the rows whose predecessor another round
     // solved (more rows than lanes), from LDS
-    if (pos[EPB_] <= cap && total > EPB_ * GL) {   // rows whose predecessor was solved in another round
+    if (!lam && pos[EPB_] <= cap && total > EPB_ * GL) {   // rows whose predecessor was solved in another round
         wave_sync();
         for (int t = lane; t < total; t += EPB_ * GL) {
             int e = 0;
@@ -956,6 +993,207 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             }
         }
     }
+}
+
+
+// f(std::integral_constant<int, k>) for k = 0 .. N-1 (an index usable as a constant expression, e.g. a DPP control)
+template <typename F, int... K>
+__device__ __attribute__((always_inline)) inline void static_for_impl(F&& f, std::integer_sequence<int, K...>) {
+    (f(std::integral_constant<int, K>{}), ...);
+}
+template <int N, typename F>
+__device__ __attribute__((always_inline)) inline void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ------------------------------------------------------------------------- PGS, Delassus form
+// The same Gauss-Seidel sweep as the velocity-form PGS below (rows in Bullet order, P.iters iterations, friction bounds
+// from the current normal impulse, nu += (M^-1 J^T)_k dl after every row update), restated so that the row-to-row
+// chain needs no reduction: the constraint velocities w = J nu are carried per row,
+//     row k:  lambda_k' = clamp(lambda_k + meff_k (b_k - w_k)),  dl = lambda_k' - lambda_k,  w += A[:, k] dl,
+// with A = J M^-1 J^T (the Delassus matrix).  Lane l of an env owns the env's rows l and l + 16 (residual b - w,
+// lambda and bounds in registers) and the generalised velocity components l and 16 + l; at step k the owner's dl reaches
+// the env's 16 lanes by one DPP row_newbcast and every lane updates its two residuals and two velocity components with
+// one fma each, reading A and M^-1 J^T four steps ahead from LDS: the chain is fma, med3, sub, broadcast, fma - no
+// 16-lane J . nu reduction per row (4 DPP adds, the velocity form's).  A is formed per substep on the matrix cores:
+// C = J (rows x 24) x (M^-1 J^T)^T by v_mfma_f32_16x16x4_f32 16 x 16 tiles (K = 23 padded with a zero), the 4 envs'
+// chains interleaved, written over the rows' J slots (J . nu* was taken by group_rows).  The rows sit back to back in
+// the pool (no zero rows): a friction row's normal is at least one step earlier, so its bound is read one step ahead.
+template <int EPB_>
+__device__ __attribute__((always_inline)) void pgs_delassus(const PhysParams& P, GroupLDS<float>* shb, GroupLDS<float>& S,
+                                                             int nl, int nc, int pbase, int l, float& n0, float& n1) {
+    static_assert(EPB_ == 4 && LMAX <= NV && LMAX <= 2 * GL, "one MFMA wave of 4 envs; a row's J slots hold its A row");
+    using f4 = float __attribute__((ext_vector_type(4)));
+    char* lds0 = reinterpret_cast<char*>(shb);
+    const int lane = threadIdx.x & 63;
+    int pe[EPB_], ne[EPB_], M = 0;
+    {
+        int acc = 0;
+#pragma unroll
+        for (int e = 0; e < EPB_; e++) {
+            pe[e] = acc;
+            ne[e] = __builtin_amdgcn_readlane(nl, e * GL) + 3 * __builtin_amdgcn_readlane(nc, e * GL);
+            acc += ne[e];
+            M = max(M, ne[e]);
+        }
+    }
+    if (M == 0) return;   // wave-uniform: no constraint row in any env
+    const bool TWOANY = M > GL;   // wave-uniform
+    const int neff = nl + 3 * nc;
+    const int dummy = (int)(reinterpret_cast<char*>(&S.nu[NV]) - lds0);   // an unused word: reads of 0, stray stores
+    // finite reads standing in for absent rows (their updates are dl = 0): the env's rotation matrices (>= 46 words)
+    const int finite = (int)(reinterpret_cast<char*>(&S.R[0][0]) - lds0);
+    if (l == 0) S.nu[NV] = 0.f;
+    // ---- A of every env: lane (lk, lr) supplies J / M^-1 J^T of row lr (+ 16) at k = 4 s + lk (rows past the env and
+    //      k = 23 masked to 0); C[4 lk + q][lr] comes back.  Every operand is read before any A entry is written.
+    const int lr = lane & 15, lk = lane >> 4;
+    using f2 = float __attribute__((ext_vector_type(2)));
+    f2 op[EPB_][2][6];
+    auto load_ops = [&](int ti) {
+#pragma unroll
+        for (int e = 0; e < EPB_; e++) {
+            const int r = lr + GL * ti;
+            const bool rv = r < ne[e];
+            const float* R = reinterpret_cast<const float*>(lds0 + (rv ? pool_off<float>(pe[e] + r) : finite));
+#pragma unroll
+            for (int s4 = 0; s4 < 6; s4++) {
+                const int k = 4 * s4 + lk;
+                const f2 jm = *reinterpret_cast<const f2*>(R + 2 * min(k, NV - 1));   // (J_k, (M^-1 J^T)_k)
+                op[e][ti][s4] = rv && k < NV ? jm : f2{0.f, 0.f};
+            }
+        }
+    };
+    load_ops(0);
+    if (TWOANY) load_ops(1);
+    PGS_SUBPHASE(19);
+    f4 c00[EPB_], c01[EPB_], c11[EPB_];
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) c00[e] = c01[e] = c11[e] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s4 = 0; s4 < 6; s4++)
+#pragma unroll
+        for (int e = 0; e < EPB_; e++)
+            c00[e] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[e][0][s4].x, op[e][0][s4].y, c00[e], 0, 0, 0);
+    if (TWOANY) {
+#pragma unroll
+        for (int s4 = 0; s4 < 6; s4++)
+#pragma unroll
+            for (int e = 0; e < EPB_; e++) {
+                c01[e] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[e][0][s4].x, op[e][1][s4].y, c01[e], 0, 0, 0);
+                c11[e] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[e][1][s4].x, op[e][1][s4].y, c11[e], 0, 0, 0);
+            }
+    }
+    PGS_SUBPHASE(20);
+    // A[r][c] into row r's J slot 2 c (rows of the env, c < LMAX; columns past the env: the zeros C holds there)
+#pragma unroll
+    for (int e = 0; e < EPB_; e++) {
+        auto put = [&](int r, int c, float v) {
+            const bool ok = r < ne[e] && c < LMAX;
+            *reinterpret_cast<float*>(lds0 + (ok ? pool_off<float>(pe[e] + r) + 2 * c * (int)sizeof(float) : dummy)) = v;
+        };
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = 4 * lk + q;
+            put(r, lr, c00[e][q]);
+        }
+        if (TWOANY) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = 4 * lk + q;
+                put(r, GL + lr, c01[e][q]);
+                put(GL + lr, r, c01[e][q]);   // A is symmetric: the (1, 0) tile is the (0, 1) one transposed
+                put(GL + r, GL + lr, c11[e][q]);
+            }
+        }
+    }
+    // ---- the lane's rows l and l + 16: residual b - J nu*, bounds, LDS offsets of its A row, its lambda and the
+    //      lambda bounding it (absent rows: zeros, the dummy word, finite stand-in reads)
+    float r0, r1, me0, me1, hi0, hi1, mu0, mu1, lam0 = 0.f, lam1 = 0.f;
+    int ao0, ao1, lno0, lno1, lmo0, lmo1;
+    {
+        auto row_in = [&](int q, float& rq, float& meq, float& hiq, float& muq, int& aoq, int& lnoq, int& lmoq) {
+            const bool v = q < neff;
+            const int off = v ? pool_off<float>(pbase + q) : finite;
+            const float* R = reinterpret_cast<const float*>(lds0 + off);
+            const f4 s0 = *reinterpret_cast<const f4*>(R + RO_S0), s1 = *reinterpret_cast<const f4*>(R + RO_S1);
+            rq = v ? s0.x - s1.y : 0.f;   // b - J nu*
+            hiq = v ? s0.y : 0.f;
+            meq = v ? s0.w : 0.f;
+            muq = v ? s1.x : 0.f;
+            lnoq = v ? __float_as_int(s1.w) : dummy;
+            lmoq = v ? off + RO_LAM * (int)sizeof(float) : dummy;
+            aoq = off;
+        };
+        row_in(l, r0, me0, hi0, mu0, ao0, lno0, lmo0);
+        row_in(GL + l, r1, me1, hi1, mu1, ao1, lno1, lmo1);
+    }
+    // the env's row k for the velocity updates: its (M^-1 J^T)_l / _(16 + l) words (absent rows: finite stand-ins)
+    const int mo0 = (2 * l + 1) * (int)sizeof(float), mo1 = (l < NV - GL ? 2 * (GL + l) + 1 : RO_Z) * (int)sizeof(float);
+    auto row_off = [&](int k) { return k < neff ? pool_off<float>(pbase + k) : finite; };
+    wave_sync();   // the A entries
+    PGS_SUBPHASE(21);
+    // one sweep over the rows; TWO: some env of the wave has rows in slot 1 (> 16 rows).  Steps come in chunks of 4
+    // straight-line steps (the wave-uniform row count is tested once per chunk: a step past an env's rows is a no-op
+    // dl = 0), so the LDS reads and writes of a chunk are counted exactly by the waitcnts
+    float v0 = n0, v1 = n1;
+    auto sweep = [&](auto two_c) {
+        constexpr bool TWO = decltype(two_c)::value;
+        constexpr int AH = 4;   // A and M^-1 J^T entries read AH steps ahead
+        float a0v[AH], a1v[AH], m0v[AH], m1v[AH], lnv = 0.f;
+        auto fetch = [&](int k, int j) {
+            a0v[j] = *reinterpret_cast<const float*>(lds0 + ao0 + 2 * k * (int)sizeof(float));
+            if constexpr (TWO) a1v[j] = *reinterpret_cast<const float*>(lds0 + ao1 + 2 * k * (int)sizeof(float));
+            const int ro = row_off(k);
+            m0v[j] = *reinterpret_cast<const float*>(lds0 + ro + mo0);
+            m1v[j] = *reinterpret_cast<const float*>(lds0 + ro + mo1);
+        };
+        static_for<AH>([&](auto jc) { fetch(decltype(jc)::value, decltype(jc)::value); });
+        static_for<(LMAX + 3) / 4>([&](auto cc) {
+            constexpr int c0 = 4 * decltype(cc)::value;
+            if (c0 >= M || (!TWO && c0 >= GL)) return;   // wave-uniform
+            static_for<4>([&](auto jc) {
+                constexpr int k = c0 + decltype(jc)::value;
+                if constexpr (k < LMAX && (TWO || k < GL)) {
+                    constexpr bool hi_slot = k >= GL;
+                    const float a0k = a0v[k % AH], a1k = TWO ? a1v[k % AH] : 0.f, m0k = m0v[k % AH], m1k = m1v[k % AH];
+                    if constexpr (k + AH < LMAX) fetch(k + AH, k % AH);
+                    const float ln = lnv;
+                    const float mu = hi_slot ? mu1 : mu0, hc = hi_slot ? hi1 : hi0, me = hi_slot ? me1 : me0;
+                    const float rr = hi_slot ? r1 : r0, lamv = hi_slot ? lam1 : lam0;
+                    const float lsol = med3(fmaf(me, rr, lamv), -(mu * ln), fmaf(mu, ln, hc));   // == clamp: lo <= hi
+                    const float dl = lsol - lamv;
+                    const int di = __float_as_int(dl);
+                    // row_newbcast: the owner's (lane k % 16 of each env) dl to its env's 16 lanes
+                    const float dlb = __int_as_float(__builtin_amdgcn_update_dpp(di, di, 0x150 + (k & (GL - 1)), 0xF, 0xF,
+                                                                                 false));
+                    const float lnew = l == (k & (GL - 1)) ? lsol : lamv;
+                    if constexpr (hi_slot) {
+                        lam1 = lnew;
+                        *reinterpret_cast<float*>(lds0 + lmo1) = lnew;
+                    } else {
+                        lam0 = lnew;
+                        *reinterpret_cast<float*>(lds0 + lmo0) = lnew;
+                    }
+                    // the bounding lambda of step k + 1 (a friction row's normal is at least one step earlier: its
+                    // lambda of this sweep was stored before)
+                    if constexpr (k + 1 < LMAX)
+                        lnv = *reinterpret_cast<const float*>(lds0 + (k + 1 < GL ? lno0 : lno1));
+                    r0 = fmaf(-a0k, dlb, r0);
+                    if constexpr (TWO) r1 = fmaf(-a1k, dlb, r1);
+                    v0 = fmaf(m0k, dlb, v0);
+                    v1 = fmaf(m1k, dlb, v1);
+                }
+            });
+        });
+    };
+#pragma unroll 1
+    for (int it = 0; it < P.iters; it++) {
+        if (TWOANY) sweep(std::true_type{});
+        else sweep(std::false_type{});
+    }
+    PGS_SUBPHASE(22);
+    n0 = v0;
+    n1 = v1;
 }
 
 // ------------------------------------------------------------------------- ABA pass 2, one tree level
@@ -1690,7 +1928,8 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     //      all EPB_ envs of the wave spread over its lanes (one round instead of max_e ceil(nrows_e / 16))
     const int nrows = nl + 3 * nc;
     int pbase, ptot;   // this env's first pool position, the block's pool positions in use
-    group_rows<T, EPB_>(P, shb, gblock, nl, nc, dt, pbase, ptot);
+    bool lam;          // the Delassus-form PGS (wave-uniform)
+    group_rows<T, EPB_>(P, shb, gblock, nl, nc, dt, pbase, ptot, lam);
     const int cap = P.lds_rows;
     WLOG(1, env_max<EPB_>(nrows));
     __syncthreads();
@@ -1709,10 +1948,19 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         }
     }
 #endif
+    bool delassus_done = false;
+    if constexpr (delassus_kernel<T, EPB_>()) {
+        if (lam) {   // wave-uniform
+            pgs_delassus<EPB_>(P, shb, S, nl, nc, pbase, l, n0, n1);
+            delassus_done = true;
+        }
+    }
+    if (delassus_done) {
+    }
 #ifndef HUM_PGS_SLOW
-    if (ptot <= cap) {   // wave-uniform
+    else if (ptot <= cap) {   // wave-uniform
 #else
-    if (false) {
+    else if (false) {
 #endif
         // Common case (the block's rows all in its LDS pool).  Gauss-Seidel over the flattened (iteration,
         // row) sequence, restated for latency: with n_k the velocity before row k and dl_k its impulse change,

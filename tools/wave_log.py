@@ -91,6 +91,9 @@ sub = X[:, 17:30]   # sub-phase markers 11-23 (HUM_SUBPHASE builds): time from t
 subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1: inertia+bias", 15: "pass3: base",
         17: "post: book load", 19: "post: calc_state", 20: "post: reward", 21: "post: target",
         22: "post: ref obs + done", 16: "post: obs row", 23: "post: rew/done/frame", 18: "post: return"}
+if os.environ.get("PGS_SUB") == "1":   # HUM_SUBPHASE_PGS builds: the Delassus PGS's split instead of the post step's
+    subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1: inertia+bias", 15: "pass3: base",
+            19: "pgs: A operands", 20: "pgs: A MFMA", 21: "pgs: A stores + rows", 22: "pgs: sweeps"}
 if sub.any():
     print("sub-phase cycles per block-step (each taken out of its phase above): mean | slowest 1%")
     for k, nm in subn.items():
