@@ -171,7 +171,8 @@ def parity_sample(env, clips, per_clip=64, seed=5, sens_bound=1e-5):
 def _actions_desc(a):
     if a.hier and a.policy:
         return ("on-GPU policies of both levels in the loop (random-init 44-256-256-2 high-level and 70-256-256-17 "
-                "low-level tanh MLPs + Gaussian exploration, hum_hier_rollout)")
+                "low-level tanh MLPs + Gaussian exploration, %s)" % ("hum_hier_rollout_fused" if a.fused
+                                                                      else "hum_hier_rollout"))
     if a.policy:
         return "on-GPU policy actions (random-init 70-256-256-17 tanh MLP + Gaussian exploration) in the loop"
     return "uniform random actions (a fresh row per env step)"
@@ -212,6 +213,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     G = a.gather_every if a.dist and not a.policy else 0
     if G and G % k:
         raise SystemExit("--gather-every must be a multiple of --k")
+    soff = [0]   # --policy: launches before the timed ones (the timed launch s is launch soff + s of the run)
     ring = [None]   # the launch's output buffers (packed into the gather fragment right after the launch)
     rem_out = {}   # output buffers of the shorter remainder launches, by size
     if a.hier:
@@ -224,16 +226,21 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             if kk < k:   # the remainder launch
                 return env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True, out=rem_out.get(kk))
             ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
-        if a.policy:   # config 5 closed loop: both levels' policies on the device (hum_hier_rollout)
-            from ilrl_amd.policy import DevicePolicy, hier_rollout
+        if a.policy:   # config 5 closed loop: both levels' policies on the device (hum_hier_rollout[_fused])
+            from ilrl_amd.policy import DevicePolicy, hier_rollout, hier_traj_buffers
             high = DevicePolicy.random_init_high(seed=17 + rank, device=dev.index)
             low = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
-            acted = []   # per launch: the agent that acted per (transition, lane), counted after the timed region
+            traj_out = {}   # by launch size: the trajectory rows, reused launch to launch (allocated before the clock)
+            acted = {}      # by launch number: the agent that acted per (transition, lane), counted after the clock
 
-            def step(s, kk=k):
-                tr = hier_rollout(env, high, low, kk, explore=True, step0=s * k, trajectories=True)
-                acted.append(tr["acted"])
-                return tr
+            def traj_bufs(kk, s):
+                o = dict(traj_out.setdefault(kk, hier_traj_buffers(n, kk, dev)))
+                o["acted"] = acted.setdefault(s + soff[0], torch.empty(kk, n, dtype=torch.uint8, device=dev))
+                return o
+
+            def step(s, kk=k):   # launch numbers (and the exploration noise's step index) continue past the warm-up
+                return hier_rollout(env, high, low, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True,
+                                    fused=a.fused, out=traj_bufs(kk, s))
             env._bench_acted = acted
     else:
         from ilrl_amd.clips import CLIP_NAMES
@@ -253,11 +260,11 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             actbuf = torch.zeros(n, 17, device=dev)
 
             def step(s, kk=1):
-                pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s, out=actbuf)
+                pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s + soff[0], out=actbuf)
                 return env.step(actbuf, autoreset=True)
             if a.fused:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
                 def step(s, kk=k):
-                    return pol.rollout(env, kk, explore=True, step0=s * k, trajectories=True, fused=True)
+                    return pol.rollout(env, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True, fused=True)
     env.reset()
     env.done.zero_()
     for w in range(wlaunches):
@@ -274,6 +281,10 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         tg = TrajectoryGather(fields, [shard(n * world, world, r)[1] for r in range(world)], G, dev)
         tg.start(0)   # communicator setup (RCCL point-to-point pairs) outside the timed region
         tg.wait()
+    soff[0] = wlaunches
+    if a.hier and a.policy:   # the timed launches' trajectory buffers
+        for s, kk in enumerate(sizes):
+            traj_bufs(kk, s)
     if not a.policy:
         # every output buffer the timed launches write exists before the clock starts (a warmup shorter than k, e.g.
         # the driver's --steps 20 --warmup 5, never ran a launch of the timed shape: its allocation and zero fill
@@ -327,7 +338,8 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     low_steps = None
     if a.hier and a.policy:   # physics env-steps in the timed region: the low-level transitions the rollouts recorded
         from ilrl_amd import _native as N
-        low_steps = float(sum(int((x == N.HUM_AGENT_LOW).sum().item()) for x in env._bench_acted[wlaunches:]))
+        low_steps = float(sum(int((env._bench_acted[wlaunches + s] == N.HUM_AGENT_LOW).sum().item())
+                              for s in range(launches)))
     elif a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
         low_steps = float(count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank))
         if a.dist:
@@ -435,12 +447,15 @@ def main():
                                    "%s, %d envs/GPU, %s, auto-reset, %s env steps per %s" % (
                                        a.clip, n, _actions_desc(a),
                                        "/".join(str(s) for s in sorted(set(sizes), reverse=True)),
-                                       "hum_hier_rollout call (2 policy launches + 1 env launch per transition)"
+                                       ("hum_hier_rollout_fused launch (both networks inside the env kernel)"
+                                        if a.fused else
+                                        "hum_hier_rollout call (2 policy launches + 1 env launch per transition)")
                                        if a.hier and a.policy else "launch"),
-                       "fused": bool(a.policy and a.fused and not a.hier),
+                       "fused": bool(a.policy and a.fused),
                        "envs_per_gpu": n, "clip": a.clip, "k": a.k,
                        # the launches the timed region actually ran (--steps < k: one shorter launch)
-                       "launches": len(sizes), "steps_per_launch": sorted(set(sizes), reverse=True),
+                       "launches": len(sizes), "steps_per_launch": max(sizes),
+                       "launch_sizes": sorted(set(sizes), reverse=True),
                        "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
             # per env step: kernel_ms = launch duration / k; achieved = the env step's algorithmic bytes over it
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

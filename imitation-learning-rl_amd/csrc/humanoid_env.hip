@@ -897,6 +897,81 @@ __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
     if (st != hipSuccess) return fail(HUM_ERR_HIP, std::string("hum_rollout_fused: ") + hipGetErrorString(st));
     return HUM_OK;
 }
+// hum_hier_rollout_fused (policy.hip): k two-level sampler transitions in one launch of the cooperative kernel with
+// both networks inside (POLICY == 2).  pw_high / pw_low: the hum_policy weight blocks.  The per-transition agents /
+// rewards / done rows go to the trajectory when given, else to the handle's scratch (grown on demand,
+// stream-ordered: every call on one handle must use one stream, or order its streams with events)
+__attribute__((visibility("hidden"))) int hum_internal_hier_rollout_fused(
+    hum_env* e, const float* pw_high, uint64_t seed_high, const float* pw_low, uint64_t seed_low, int32_t k,
+    int32_t explore, uint64_t step0, const hum_hier_io* io, const hum_hier_traj* T, void* stream) {
+    if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != 4 || e->terrain != HUM_TERRAIN_PLANE ||
+        !e->cfg.hier)
+        return fail(HUM_ERR_STATE, "hum_hier_rollout_fused: needs a hierarchical handle on the cooperative fp32 kernel, "
+                                   "4 envs per block and plane ground (use hum_hier_rollout)");
+    if (!any_clip(e)) return fail(HUM_ERR_NOCLIP, "hum_hier_rollout_fused: no clip uploaded (hum_set_clip)");
+    HIPCHK(hipSetDevice(e->cfg.device));
+    const hipStream_t s = stream_of(e, stream);
+    const size_t n = (size_t)e->n, kn = (size_t)k * n;
+    float* rh = T->rew_high;
+    float* rl = T->rew_low;
+    uint8_t* ag = T->agents;
+    uint8_t* dn = T->done;
+    if (!rh || !rl || !ag || !dn) {
+        const size_t fb = (kn * sizeof(float) + 255) / 256 * 256, bb = (kn + 255) / 256 * 256, need = 2 * fb + 2 * bb;
+        if (need > e->traj_bytes) {   // the previous launches using it are ordered before the free on this stream
+            HIPCHK(hipStreamSynchronize(s));
+            if (e->traj) HIPCHK(hipFree(e->traj));
+            e->traj = nullptr;
+            e->traj_bytes = 0;
+            HIPCHK(hipMalloc(&e->traj, need));
+            e->traj_bytes = need;
+        }
+        char* base = (char*)e->traj;
+        if (!rh) rh = (float*)base;
+        if (!rl) rl = (float*)(base + fb);
+        if (!ag) ag = (uint8_t*)(base + 2 * fb);
+        if (!dn) dn = (uint8_t*)(base + 2 * fb + bb);
+    }
+    KArgs a = make_args(e);
+    a.flags = HUM_STEP_AUTORESET;
+    a.ksteps = k;
+    a.obs = io->obs_low;
+    a.obs_high = io->obs_high;
+    a.obs_high_reset = io->obs_high_reset;
+    a.done_in = io->done;
+    a.rew = rl;
+    a.rew_high = rh;
+    a.agents = ag;
+    a.done = dn;
+    a.acted = T->acted;
+    a.pw = pw_low;
+    a.pseed = seed_low;
+    a.obs_traj = T->obs_low;
+    a.act_traj = T->act_low;
+    a.act_last = io->act_low;
+    a.pw_high = pw_high;
+    a.pseed_high = seed_high;
+    a.obs_traj_high = T->obs_high;
+    a.act_traj_high = T->act_high;
+    a.act_last_high = io->act_high;
+    a.pstep0 = step0;
+    a.pexplore = explore;
+    const int nb = (e->n + 3) / 4;
+#ifndef HUM_DIAG_F32_ONLY
+    hipError_t st = launch_group_f32_4_hier_policy(a, nb, s);
+#else
+    (void)nb;
+    hipError_t st = hipErrorInvalidDeviceFunction;
+#endif
+    // the last transition's rows into the env buffers
+    const size_t last = (size_t)(k - 1) * n;
+    if (st == hipSuccess) st = hipMemcpyAsync(io->agents, ag + last, n, hipMemcpyDeviceToDevice, s);
+    if (st == hipSuccess) st = hipMemcpyAsync(io->rew_high, rh + last, n * sizeof(float), hipMemcpyDeviceToDevice, s);
+    if (st == hipSuccess) st = hipMemcpyAsync(io->rew_low, rl + last, n * sizeof(float), hipMemcpyDeviceToDevice, s);
+    if (st == hipSuccess) st = hipMemcpyAsync(io->done, dn + last, n, hipMemcpyDeviceToDevice, s);
+    if (st != hipSuccess) return fail(HUM_ERR_HIP, std::string("hum_hier_rollout_fused: ") + hipGetErrorString(st));
+    return HUM_OK;
+}
 // one hierarchical transition (hum_hier_step, agent = each lane's expected one) that also records the agent that
 // acted per lane (acted [n], may be NULL): hum_hier_rollout's env launch (policy.hip)
 __attribute__((visibility("hidden"))) int hum_internal_hier_step_acted(

@@ -81,6 +81,15 @@ struct KArgs {
     // hierarchical env, optional [ksteps, n]: the agent that acted in each transition (HUM_AGENT_HIGH / _LOW; 0 = the
     // lane was not stepped: no action for it, or a non-finite low-level action) - hum_hier_rollout's trajectory
     unsigned char* acted;
+    // fused two-level rollout (hum_hier_rollout_fused, the POLICY == 2 kernel): the high-level network (the same
+    // block layout at 44 -> 2) and its seed / trace rows; the low level uses pw / pseed / obs_traj / act_traj /
+    // act_last above.  The [n, ...] observation buffers (obs, obs_high, obs_high_reset) are then updated in place
+    // (row i) rather than per step, exactly as the step-by-step loop's env buffers are.
+    const float* pw_high;
+    unsigned long long pseed_high;
+    float* obs_traj_high;
+    float* act_traj_high;
+    float* act_last_high;
 };
 
 // CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
@@ -467,7 +476,11 @@ __device__ inline float hier_update_reward_high(Book& b) {
 // physics of a low step; stores state/book and writes the dict-shaped outputs.
 template <typename T>
 __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, long io, T* st, Book& b, bool high, unsigned& ef,
-                                                          const T* scs = nullptr, bool store_state = true) {
+                                                          const T* scs = nullptr, bool store_state = true, long ro = -1,
+                                                          const float* lact = nullptr, const float* hact = nullptr) {
+    // ro: the row of the [.., n, 44/70] observation outputs (default the step's row io; the fused rollout's
+    // in-place [n, ...] buffers: i); lact / hact: the step's low / high actions in registers (default a.act / a.act_high)
+    if (ro < 0) ro = io;
     const ClipDev& c = a.clips[b.clip];
     b.robot_pos[0] = b.bxy[0]; b.robot_pos[1] = b.bxy[1]; b.robot_pos[2] = 0;   // step(): :358-361
     float obs[HUM_NOBS], js[NDOF], o44[HUM_NOBS_HIGH];
@@ -479,7 +492,7 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     if (high) {
         // cur_obs is the last calc_state (same physics state, walk target before this call)
         calc_state(st, b.wt, obs, js, jal, pp);
-        const float a0 = a.act_high[2 * io], a1 = a.act_high[2 * io + 1];
+        const float a0 = hact ? hact[0] : a.act_high[2 * io], a1 = hact ? hact[1] : a.act_high[2 * io + 1];
         const float actionDegree = (float)atan2((double)a1, (double)a0) * (float)RAD2DEG;   // :540 (float32)
         const double newDegree = (double)actionDegree + pp.yaw * RAD2DEG;                   // :543
         b.hldt = newDegree * DEG2RAD;
@@ -500,7 +513,7 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     } else {
         b.level_rem -= 1;                                                                   // :584
         calc_state(st, b.wt, obs, js, jal, pp, scs);                                        // :591
-        const float* act = a.act + io * HUM_NACT;
+        const float* act = lact ? lact : a.act + io * HUM_NACT;
         // updateReward (:494-522)
         double dJ = 0, dV = 0;
 #pragma unroll
@@ -583,11 +596,11 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     }
     if (agents & HUM_AGENT_LOW) {
 #pragma unroll
-        for (int k = 0; k < HUM_NOBS; k++) a.obs[io * HUM_NOBS + k] = obs[k];
+        for (int k = 0; k < HUM_NOBS; k++) a.obs[ro * HUM_NOBS + k] = obs[k];
     }
     if (agents & HUM_AGENT_HIGH) {
 #pragma unroll
-        for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high[io * HUM_NOBS_HIGH + k] = o44[k];
+        for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high[ro * HUM_NOBS_HIGH + k] = o44[k];
     }
     a.rew[io] = (agents & HUM_AGENT_LOW) ? rew_low : 0.f;   // the level hand-back drops the low reward (:631-636)
     a.rew_high[io] = rew_high;
@@ -599,7 +612,7 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
         hier_reset_lane(a, i, st, b, -1, 0.0, r44, ef);
         if (a.obs_high_reset) {
 #pragma unroll
-            for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high_reset[io * HUM_NOBS_HIGH + k] = r44[k];
+            for (int k = 0; k < HUM_NOBS_HIGH; k++) a.obs_high_reset[ro * HUM_NOBS_HIGH + k] = r44[k];
         }
     }
     if (store_state) store_lane(a, i, st, b);
@@ -741,27 +754,38 @@ __device__ __attribute__((always_inline)) inline void policy_hidden(HUM_LDS floa
 #pragma unroll
         for (int m = 0; m < 4; m++) F[e][dst + 4 * lane + m] = tanhf(acc[e][m] + bias[m]);
 }
-template <typename T, int EPB_>
-__device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, GroupLDS<T>* sh, int blk, int t) {
+// NIN -> 256 -> 256 -> NOUT: the low-level network (70 -> 17, weights pw, seed pseed) or the hierarchical env's
+// high-level one (44 -> 2); emask: bit GL e set = env e of the wave acts with this network (the others' results are
+// dropped: a wave whose envs expect different agents runs both networks, each keeping its own envs' actions)
+template <typename T, int EPB_, int NIN = HUM_NOBS, int NOUT = HUM_NACT>
+__device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, GroupLDS<T>* sh, int blk, int t, const float* pw,
+                                                           unsigned long long pseed, unsigned long long emask,
+                                                           float* act_traj, float* act_last) {
     static_assert(EPB_ * 16 == 64, "policy_wave: one (env, column) chain per lane");
+    static_assert(NOUT == 17 || NOUT * EPB_ <= 64, "policy_wave: output chains");
     const int lane = threadIdx.x & 63;
-    const HUM_GLOBAL float* W1 = (const HUM_GLOBAL float*)a.pw;
+    const HUM_GLOBAL float* W1 = (const HUM_GLOBAL float*)pw;
     const HUM_GLOBAL float* B1 = W1 + 72 * 256;
     const HUM_GLOBAL float* W2 = B1 + 256;
     const HUM_GLOBAL float* B2 = W2 + 256 * 256;
     const HUM_GLOBAL float* W3 = B2 + 256;
-    const HUM_GLOBAL float* B3 = W3 + 256 * HUM_NACT;
-    const HUM_GLOBAL float* LSTD = B3 + HUM_NACT;
+    const HUM_GLOBAL float* B3 = W3 + 256 * NOUT;
+    const HUM_GLOBAL float* LSTD = B3 + NOUT;
     HUM_LDS float* F[EPB_];   // LDS-typed: no generic (flat) access
 #pragma unroll
     for (int e = 0; e < EPB_; e++) F[e] = (HUM_LDS float*)policy_scratch(sh[e]);
-    // hidden layer 1 (K = 70: policy.hip's zero rows 70, 71 add exact zeros), hidden layer 2
-    policy_hidden<EPB_, HUM_NOBS, 10>(F, W1, B1, PX_OFF, PH1_OFF, lane);
+    // hidden layer 1 (K = NIN: policy.hip's zero rows NIN .. 71 add exact zeros), hidden layer 2
+    policy_hidden<EPB_, NIN, (NIN % 10 == 0 ? 10 : 11)>(F, W1, B1, PX_OFF, PH1_OFF, lane);
     wave_sync();
     policy_hidden<EPB_, 256, 16>(F, W2, B2, PH1_OFF, PH2_OFF, lane);
     wave_sync();
-    // output layer: chain A = (env lane / 16, column lane % 16), chain B = (env lane, column 16) in lanes < EPB_
-    const int eA = lane >> 4, cA = lane & 15, eB = lane < EPB_ ? lane : 0;
+    // output layer: 17 wide: chain A = (env lane / 16, column lane % 16), chain B = (env lane, column 16) in lanes
+    // < EPB_; narrower: chain A = (env lane / NOUT, column lane % NOUT) in lanes < EPB_ NOUT
+    constexpr bool WIDE = NOUT == 17;
+    const int eA = WIDE ? lane >> 4 : (lane < EPB_ * NOUT ? lane / NOUT : 0);
+    const int cA = WIDE ? lane & 15 : (lane < EPB_ * NOUT ? lane % NOUT : 0);
+    const bool onA = WIDE || lane < EPB_ * NOUT;
+    const int eB = lane < EPB_ ? lane : 0;
     const HUM_LDS float* hA = F[0] + PH2_OFF;
     const HUM_LDS float* hB = F[0] + PH2_OFF;
 #pragma unroll
@@ -772,17 +796,18 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
     float accA = 0.f, accB = 0.f;
 #pragma unroll 16
     for (int k = 0; k < 256; k++) {
-        const HUM_GLOBAL float* wr = W3 + k * HUM_NACT;
+        const HUM_GLOBAL float* wr = W3 + k * NOUT;
         accA = fmaf(hA[k], wr[cA], accA);
-        accB = fmaf(hB[k], wr[16], accB);
+        if constexpr (WIDE) accB = fmaf(hB[k], wr[16], accB);
     }
     // + DiagGaussian sample + clip_actions
     auto finish = [&](int e, int c, float acc) {
+        if (!((emask >> (GL * e)) & 1ull)) return;
         const float mean = acc + B3[c];
         float v = mean;
         const int i = blk * EPB_ + e;
         if (a.pexplore) {   // policy.hip: (seed, lane, step, column) through separate mixing rounds, Box-Muller
-            const unsigned long long x = pmix64(pmix64(pmix64(a.pseed ^ (unsigned long long)i) ^ (a.pstep0 + t)) ^
+            const unsigned long long x = pmix64(pmix64(pmix64(pseed ^ (unsigned long long)i) ^ (a.pstep0 + t)) ^
                                                 (unsigned long long)c);
             const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;
             const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
@@ -794,12 +819,12 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
         pa[c] = fminf(fmaxf(v, -1.f), 1.f);
         if (i < a.n) {
             const long io = (long)t * a.n + i;
-            if (a.act_traj) a.act_traj[io * HUM_NACT + c] = v;   // the sample before clip_actions (SampleBatch)
-            if (a.act_last && t == a.ksteps - 1) a.act_last[(long)i * HUM_NACT + c] = pa[c];
+            if (act_traj) act_traj[io * NOUT + c] = v;   // the sample before clip_actions (SampleBatch)
+            if (act_last && t == a.ksteps - 1) act_last[(long)i * NOUT + c] = pa[c];
         }
     };
-    finish(eA, cA, accA);
-    if (lane < EPB_) finish(eB, 16, accB);
+    if (onA) finish(eA, cA, accA);
+    if (WIDE && lane < EPB_) finish(eB, 16, accB);
     wave_sync();
 }
 
@@ -809,7 +834,9 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
 #ifndef HUM_GROUP_MIN_WAVES
 #define HUM_GROUP_MIN_WAVES 1
 #endif
-template <typename T, int EPB_, bool TERRAIN = false, bool POLICY = false>
+// POLICY: 0 = actions from a.act (hum_step_k / hum_hier_step_k), 1 = the low-level network inside the step loop
+// (hum_rollout_fused), 2 = both networks of the hierarchical env (hum_hier_rollout_fused)
+template <typename T, int EPB_, bool TERRAIN = false, int POLICY = 0>
 __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a0) {
     __shared__ GroupLDS<T> sh[EPB_];
     const int ksteps = a0.ksteps;
@@ -863,7 +890,45 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     int* carry = reinterpret_cast<int*>(&S.tau[NDOF]);
     const int gbit = (tid & 63) & ~(GL - 1);
     const long io = (long)t * a.n + i;   // this step's input / output row of the env
-    if constexpr (POLICY) {
+    constexpr bool HP = POLICY == 2;
+    const bool hier = HP || a.hier;
+    if constexpr (HP) {
+        // the two-level sampler's input (hum_hier_rollout's per-transition policy calls): an env expecting the high
+        // agent reads its latest high observation (done at the previous transition: its auto-reset one), the others
+        // their latest low observation - the handle's [n, ...] rows, updated in place by the previous step's lane 0
+        float* X = policy_scratch(S) + PX_OFF;
+        const bool hi = valid && carry[0] != 0;
+        const bool dprev = valid && (t == 0 ? (a.done_in && a.done_in[i]) : a.done[io - a.n] != 0);
+        const HUM_GLOBAL float* src = nullptr;
+        if (valid)
+            src = (const HUM_GLOBAL float*)(hi ? (dprev ? a.obs_high_reset : a.obs_high) + (long)i * HUM_NOBS_HIGH
+                                               : a.obs + (long)i * HUM_NOBS);
+        const int nin = hi ? HUM_NOBS_HIGH : HUM_NOBS;
+        float xv[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const int k = l + GL * j;
+            xv[j] = (valid && k < nin) ? src[k] : 0.f;
+        }
+        HUM_GLOBAL float* trow = nullptr;
+        if (valid) {
+            if (hi && a.obs_traj_high) trow = (HUM_GLOBAL float*)(a.obs_traj_high + io * HUM_NOBS_HIGH);
+            if (!hi && a.obs_traj) trow = (HUM_GLOBAL float*)(a.obs_traj + io * HUM_NOBS);
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const int k = l + GL * j;
+            if (k < HUM_NOBS) X[k] = xv[j];
+            if (trow && k < nin) trow[k] = xv[j];
+        }
+        wave_sync();
+        // each network only for the envs that act with it; a network no env of the wave needs is skipped
+        const unsigned long long hm = __ballot(l == 0 && hi), lm = __ballot(l == 0 && valid && !hi);
+        if (hm) policy_wave<T, EPB_, HUM_NOBS_HIGH, HUM_NACT_HIGH>(a, sh, blk, t, a.pw_high, a.pseed_high, hm,
+                                                                    a.act_traj_high, a.act_last_high);
+        if (lm) policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, lm, a.act_traj, a.act_last);
+    } else if constexpr (POLICY == 1) {
         // the sampler's input: step 0 the handle's current observation (a lane done at the previous step: its reset
         // observation), later steps the row the previous step staged (its reset row if it reset)
         float* X = policy_scratch(S) + PX_OFF;
@@ -895,12 +960,12 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             }
         }
         wave_sync();
-        policy_wave<T, EPB_>(a, sh, blk, t);
+        policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, ~0ull, a.act_traj, a.act_last);
     }
     // POLICY: the env's clipped actions held in registers across the physics (which reuses the scratch), one per lane
     // (lane 0 also the 17th); post_step reads them back from LDS for the electricity cost
     float pact0 = 0.f, pact1 = 0.f;
-    if constexpr (POLICY) {
+    if constexpr (POLICY != 0) {
         pact0 = policy_scratch(S)[PACT_OFF + l];
         pact1 = policy_scratch(S)[PACT_OFF + GL];
     }
@@ -911,9 +976,9 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         S.tau[M.act_dof[k]] = (T)motor_torque(a.np1, M.act_gain[k], M.act_gain_d[k], isfinite(av) ? av : 0.f);
     }
     // hierarchical env: envs whose acting agent is the high level take no physics step (hier_env.py:538-571)
-    const unsigned char sel = a.hier && valid && a.agent_sel ? a.agent_sel[io] : (unsigned char)0;
-    const bool skip = a.hier && valid && a.agent_sel && sel == HUM_AGENT_SEL_SKIP;   // no action: lane untouched
-    const bool high = a.hier && valid && !skip && (a.agent_sel ? sel != 0 : carry[0] != 0);
+    const unsigned char sel = hier && valid && a.agent_sel ? a.agent_sel[io] : (unsigned char)0;
+    const bool skip = hier && valid && a.agent_sel && sel == HUM_AGENT_SEL_SKIP;   // no action: lane untouched
+    const bool high = hier && valid && !skip && (a.agent_sel ? sel != 0 : carry[0] != 0);
     const bool env_ok = high || ((__ballot(!fin) >> gbit) & 0xFFFFull) == 0;
     // an env that takes no physics step this round rides along with the wave's physics and keeps its LDS state
     const bool frozen = !valid || skip || high || !env_ok;
@@ -943,7 +1008,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     float* rstage = reinterpret_cast<float*>(scs + 144);   // the auto-reset observation
     static_assert(sizeof(sh[0].x.aba.IA) >= (144 + HUM_NOBS) * sizeof(T) && 2 * NDOF + 2 + 2 * NDOF <= 72,
                   "output row staging");
-    if constexpr (POLICY) {   // the step's actions for post_step, in the reset-obs staging row (written after it)
+    if constexpr (POLICY != 0) {   // the step's actions for post_step, in the reset-obs staging row (written after it)
         rstage[l] = pact0;
         if (l == 0) rstage[GL] = pact1;
     }
@@ -952,7 +1017,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     float* jstage = reinterpret_cast<float*>(scs + 216);
     static_assert(sizeof(sh[0].x.aba.IA) >= (216 + NDOF) * sizeof(T), "joint speed staging");
     int jal_l = 0;
-    if (!a.hier) {
+    if (!hier) {
         unsigned jmask = 0;
         for (int d = l; d < NDOF; d += GL) {
             float rp, rv;
@@ -973,17 +1038,24 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     if (valid && l == 0 && skip) {
         a.agents[io] = 0;
     } else if (valid && l == 0) {
-        load_book(a, i, b, a.hier != 0);
+        load_book(a, i, b, hier);
         POST_SUBPHASE(17);
         if (!env_ok) {   // humanoid.py:55 assert: env not stepped, flagged for the host
             ef |= HUM_EFLAG_NONFINITE_ACTION;
-            nonfinite_outputs(a, io, b.frame, a.hier ? nullptr : ostage);
+            nonfinite_outputs(a, io, b.frame, hier ? nullptr : ostage);
         } else {
             // the env's current state (a frozen env's: unchanged by the wave's physics)
 #pragma unroll
             for (int e = 0; e < HUM_NSTATE; e++) st[e] = S.st[e];
             booked = true;
-            if (a.hier) {
+            if (HP) {   // the actions out of the staging row into registers; observation rows in place (row i)
+                float lact[HUM_NACT];
+#pragma unroll
+                for (int k = 0; k < HUM_NACT; k++) lact[k] = rstage[k];
+                hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs, false, (long)i, lact, lact);
+#pragma unroll
+                for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];   // an auto-reset replaced it
+            } else if (a.hier) {
                 hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs, false);
 #pragma unroll
                 for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];   // an auto-reset replaced it
@@ -996,7 +1068,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         }
     }
     POST_SUBPHASE(18);
-    if (!a.hier) {
+    if (!hier) {
         // auto-reset (low-level env): lane 0 draws the start frame (reset_lane's first draw), the env's lanes
         // compute the reset pose's hinge sin / cos, lane 0 finishes reset_lane with them
         int* xch = reinterpret_cast<int*>(scs + 2 * NDOF);
@@ -1052,7 +1124,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     }
     PHASE(10);
     if (valid && l == 0 && booked) {   // the per-env integers the next step's lanes read
-        carry[0] = a.hier ? b.expect_high : 0;
+        carry[0] = hier ? b.expect_high : 0;
         carry[1] = (int)(unsigned)(b.terrain_key & 0xffffffffull);
         carry[2] = (int)(unsigned)(b.terrain_key >> 32);
     }
@@ -1214,5 +1286,6 @@ __global__ void parts_kernel(KArgs a, double* out) {
 // the benchmarked cooperative kernel lives in its own translation unit (group_f32.hip)
 hipError_t launch_group_f32_4(const KArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_group_f32_4_policy(const KArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_group_f32_4_hier_policy(const KArgs& a, int nblocks, hipStream_t s);
 
 }  // namespace hkk

@@ -31,6 +31,9 @@ int hum_internal_rollout_fused(hum_env* e, const float* pw, uint64_t seed, int32
 int hum_internal_hier_step_acted(hum_env* e, const float* high_act, const float* low_act, uint8_t* agents,
                                  float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done,
                                  uint32_t flags, float* high_obs_reset, uint8_t* acted, void* stream);
+int hum_internal_hier_rollout_fused(hum_env* e, const float* pw_high, uint64_t seed_high, const float* pw_low,
+                                    uint64_t seed_low, int32_t k, int32_t explore, uint64_t step0, const hum_hier_io* io,
+                                    const hum_hier_traj* T, void* stream);
 
 namespace {
 
@@ -307,16 +310,27 @@ int hum_rollout_fused(hum_env* env, hum_policy* p, int32_t k, int32_t explore, u
                                       obs_traj, act_traj, rew_traj, done_traj, stream);
 }
 
-int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
-                     const hum_hier_io* io, const hum_hier_traj* tr, void* stream) {
-    if (!env || !high || !low || k <= 0 || !io) return perr(HUM_ERR_ARG, "hum_hier_rollout: bad argument");
+}  // extern "C"
+namespace {
+// the argument checks hum_hier_rollout and hum_hier_rollout_fused share
+int hier_rollout_check(const char* fn, hum_env* env, hum_policy* high, hum_policy* low, int32_t k, const hum_hier_io* io) {
+    const std::string f(fn);
+    if (!env || !high || !low || k <= 0 || !io) return perr(HUM_ERR_ARG, f + ": bad argument");
     if (!io->obs_high || !io->obs_high_reset || !io->obs_low || !io->done || !io->agents || !io->rew_high ||
         !io->rew_low || !io->act_high || !io->act_low)
-        return perr(HUM_ERR_ARG, "hum_hier_rollout: every hum_hier_io buffer is required");
+        return perr(HUM_ERR_ARG, f + ": every hum_hier_io buffer is required");
     if (high->n_in != HUM_NOBS_HIGH || high->n_out != HUM_NACT_HIGH || low->n_in != HUM_NOBS || low->n_out != HUM_NACT)
-        return perr(HUM_ERR_ARG, "hum_hier_rollout: needs a (44, 2) high-level and a (70, 17) low-level policy");
+        return perr(HUM_ERR_ARG, f + ": needs a (44, 2) high-level and a (70, 17) low-level policy");
     if (hum_internal_device(env) != high->device || hum_internal_device(env) != low->device)
-        return perr(HUM_ERR_ARG, "hum_hier_rollout: the env handle and the policies are on different devices");
+        return perr(HUM_ERR_ARG, f + ": the env handle and the policies are on different devices");
+    return HUM_OK;
+}
+}  // namespace
+extern "C" {
+
+int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
+                     const hum_hier_io* io, const hum_hier_traj* tr, void* stream) {
+    if (const int rc = hier_rollout_check("hum_hier_rollout", env, high, low, k, io)) return rc;
     const hum_hier_traj none = {};
     const hum_hier_traj& T = tr ? *tr : none;
     const size_t n = (size_t)hum_num_lanes(env);
@@ -353,6 +367,16 @@ int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k,
         if (c.src && hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
             return perr(HUM_ERR_HIP, "hum_hier_rollout: copy of the last transition's rows");
     return HUM_OK;
+}
+
+// hum_hier_rollout in one launch: both networks inside the cooperative kernel's step loop, each evaluated only for
+// the envs that act with it (a wave whose four envs all expect the low agent skips the high network and vice versa)
+int hum_hier_rollout_fused(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
+                           const hum_hier_io* io, const hum_hier_traj* tr, void* stream) {
+    if (const int rc = hier_rollout_check("hum_hier_rollout_fused", env, high, low, k, io)) return rc;
+    const hum_hier_traj none = {};
+    return hum_internal_hier_rollout_fused(env, high->w, high->seed, low->w, low->seed, k, explore, step0, io,
+                                           tr ? tr : &none, stream);
 }
 
 }  // extern "C"

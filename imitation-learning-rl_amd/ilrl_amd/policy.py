@@ -143,13 +143,30 @@ class DevicePolicy:
         return tr
 
 
-def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True):
+def _hier_traj_shapes():
+    import torch as t
+    f32, u8 = t.float32, t.uint8
+    return {"acted": ((), u8), "obs_high": ((N.HUM_NOBS_HIGH,), f32), "act_high": ((N.HUM_NACT_HIGH,), f32),
+            "obs_low": ((N.HUM_NOBS,), f32), "act_low": ((N.HUM_NACT,), f32), "agents": ((), u8),
+            "rew_high": ((), f32), "rew_low": ((), f32), "done": ((), u8)}
+
+
+def hier_traj_buffers(n, k, device):
+    """Fresh trajectory tensors for hier_rollout(..., out=...) of k transitions on n lanes."""
+    import torch as t
+    return {f: t.empty((k, n) + sh, dtype=dt, device=device) for f, (sh, dt) in _hier_traj_shapes().items()}
+
+
+def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True, fused=False, out=None):
     """k transitions of the two-level env venv (a HierVecEnv after reset()) with the high-level policy `high`
     (44 -> 2) and the low-level policy `low` (70 -> 17), all on the device (hum_hier_rollout): per transition each
     lane steps with the action of the agent it expects.  venv's buffers carry the state between calls (obs_high /
     obs_high_reset / obs / done / agents / rewards).  Returns the trajectory {acted [k,n] (HUM_AGENT_HIGH / _LOW),
     obs_high [k,n,44], act_high [k,n,2], obs_low [k,n,70], act_low [k,n,17] (raw samples), agents [k,n],
-    rew_high [k,n], rew_low [k,n], done [k,n]} (or {})."""
+    rew_high [k,n], rew_low [k,n], done [k,n]} (or {}).
+    fused: one launch with both networks inside the env kernel (hum_hier_rollout_fused; the obs / act rows of the
+    agent that did not act on a lane are left unwritten).  out: a dict of the same tensors to write into (reused
+    across calls, e.g. by a timed loop) instead of fresh ones."""
     import torch as t
     n, dev = venv.n, venv.device
     if not hasattr(venv, "_act_high_buf"):
@@ -157,21 +174,22 @@ def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True):
         venv._act_low_buf = t.zeros(n, N.HUM_NACT, dtype=t.float32, device=dev)
     tr = {}
     if trajectories:
-        f32, u8 = t.float32, t.uint8
-        tr = {"acted": t.empty(k, n, dtype=u8, device=dev),
-              "obs_high": t.empty(k, n, N.HUM_NOBS_HIGH, dtype=f32, device=dev),
-              "act_high": t.empty(k, n, N.HUM_NACT_HIGH, dtype=f32, device=dev),
-              "obs_low": t.empty(k, n, N.HUM_NOBS, dtype=f32, device=dev),
-              "act_low": t.empty(k, n, N.HUM_NACT, dtype=f32, device=dev),
-              "agents": t.empty(k, n, dtype=u8, device=dev), "rew_high": t.empty(k, n, dtype=f32, device=dev),
-              "rew_low": t.empty(k, n, dtype=f32, device=dev), "done": t.empty(k, n, dtype=u8, device=dev)}
+        for f, (sh, dt) in _hier_traj_shapes().items():
+            x = out.get(f) if out else None
+            if x is None:
+                x = t.empty((k, n) + sh, dtype=dt, device=dev)
+            elif tuple(x.shape) != (k, n) + sh or x.dtype != dt or x.device != dev or not x.is_contiguous():
+                raise ValueError("hier_rollout: out[%r] must be a contiguous %s tensor of shape %s on %s"
+                                 % (f, dt, (k, n) + sh, dev))
+            tr[f] = x
     p = lambda x: x.data_ptr() if x is not None else None
     io = N.HumHierIO(p(venv.obs_high), p(venv.obs_high_reset), p(venv.obs), p(venv.done), p(venv.agents),
                      p(venv.reward_high), p(venv.reward), p(venv._act_high_buf), p(venv._act_low_buf))
     traj = N.HumHierTraj(*[p(tr.get(f)) for f, _ in N.HumHierTraj._fields_]) if trajectories else None
-    N.check(N.lib().hum_hier_rollout(venv.h, high.h, low.h, k, int(bool(explore)), ctypes.c_uint64(step0),
-                                     ctypes.byref(io), ctypes.byref(traj) if traj is not None else None,
-                                     venv._stream()), "hum_hier_rollout")
+    fn = "hum_hier_rollout_fused" if fused else "hum_hier_rollout"
+    N.check(getattr(N.lib(), fn)(venv.h, high.h, low.h, k, int(bool(explore)), ctypes.c_uint64(step0),
+                                 ctypes.byref(io), ctypes.byref(traj) if traj is not None else None,
+                                 venv._stream()), fn)
     return tr
 
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 11
+#define HUM_ABI_VERSION 12
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -61,7 +61,10 @@ extern "C" {
 #define HUM_STEP_CHECK_FINITE 8u  /* wait for the launch and return HUM_ERR_ARG if a lane's action was non-finite
                                      (humanoid.py:55 `assert np.isfinite(a).all()`; those lanes are not stepped and
                                      the sticky HUM_EFLAG_NONFINITE_ACTION bit is consumed).  Without it the launch
-                                     stays asynchronous and only the sticky bit records the event. */
+                                     stays asynchronous and only the sticky bit records the event.  A checked call
+                                     clears that bit before its launch: a non-finite action of an EARLIER unchecked
+                                     call that hum_get_error_flags has not yet reported is consumed with it (read
+                                     the flags first to keep it); the other bits stay sticky. */
 
 /* hum_reset_ex / hum_hier_reset_ex flags: resetFromFrame(startFromRef, initVel) (low_level_env.py:247-305,
  * hier_env.py:259-319); both False-able independently, default (0) = True, True as reset() uses */
@@ -350,7 +353,9 @@ int hum_rollout(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, ui
  * clipped actions; obs / done / reward end as the last step left them) with one difference: obs_reset receives
  * the reset observation of the lanes done at the LAST step only (hum_rollout writes it at every step's resets;
  * inside the launch a reset lane's new observation goes straight to the next step's policy and into obs_traj).
- * Without rew_traj / done_traj the per-step rows go to scratch kept on the handle (grown on demand, no sync).  The policy arithmetic is the
+ * Without rew_traj / done_traj the per-step rows go to scratch kept on the handle (grown on demand, no sync; the
+ * scratch is ordered on the call's stream only, so every call on one handle must use one stream, or the caller
+ * orders its streams with events).  The policy arithmetic is the
  * same k-ordered fp32 fma chains; the physics is the benchmarked kernel's.  Needs a handle with the cooperative fp32
  * kernel, 4 envs per block, plane ground and the low-level env (HUM_ERR_STATE otherwise: use hum_rollout).
  * Replaces: the RLlib sampler's compute_actions -> env.step loop (train_config.py:107-111, low_level_env.py:475). */
@@ -394,6 +399,18 @@ typedef struct {
  * Replaces: RLlib's multi-agent sampler loop over HierarchicalHumanoidEnv (Train Ray RLLib Hierarchical.py:48-88). */
 int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
                      const hum_hier_io* io, const hum_hier_traj* traj, void* stream);
+/* hum_hier_rollout in ONE launch: both networks run inside the cooperative kernel's step loop, each only for the
+ * lanes whose expected agent it is.  Equal, bitwise, to hum_hier_rollout on everything the acting agent produces:
+ * the acting agent's trajectory rows (obs / act of the high or the low policy, per `acted`), agents, both rewards,
+ * done, acted, the env buffers' observations and the final state.  Differences: trajectory rows of the agent that
+ * did NOT act on a lane are left unwritten (hum_hier_rollout evaluates both networks on every lane and records
+ * both), and io->act_high / io->act_low receive the last transition's clipped action of the acting agent only (the
+ * other agent's row keeps its previous content).  Needs the cooperative fp32 kernel (hum_config.kernel = 1,
+ * precision fp32, envs_per_block 4) and plane ground (HUM_ERR_STATE otherwise: use hum_hier_rollout).  Missing
+ * agents / reward / done trajectory rows go to the handle's scratch, which is stream-ordered: every call on one
+ * handle must use one stream (or order its streams with events). */
+int hum_hier_rollout_fused(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore,
+                           uint64_t step0, const hum_hier_io* io, const hum_hier_traj* traj, void* stream);
 
 /* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
 int hum_get_aux(hum_env* env, float* aux_out, void* stream);

@@ -57,7 +57,7 @@ def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, ever
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     print("bench line:", json.dumps({x: line[x] for x in ("value", "ms_per_step", "n_gpus", "gather")}))
-    assert line["n_gpus"] == ranks and line["config"]["steps_per_launch"] == [k]
+    assert line["n_gpus"] == ranks and line["config"]["steps_per_launch"] == k and line["config"]["launch_sizes"] == [k]
     assert line["config"]["launches"] == steps // k
     assert line["gather"]["every"] == every and line["gather"]["fragments"] == steps // every
     assert line["gather"]["backend"] == backend

@@ -220,6 +220,66 @@ def test_hier_rollout_equals_python_loop():
     low.close()
 
 
+@pytest.mark.parametrize("n,k", [(510, 20), (512, 1)])
+def test_hier_rollout_fused_equals_hier_rollout(n, k):
+    """hum_hier_rollout_fused (both networks inside the env kernel, each only for the lanes that act with it) ==
+    hum_hier_rollout bitwise on everything the acting agent produces: its policy inputs and raw samples, acted,
+    agents, both rewards, done, the env buffers and the final state.  Both envs are first driven through the same
+    unfused rollouts so lanes are out of phase (waves whose four envs expect different agents run both networks);
+    n = 510 leaves the last wave two envs short."""
+    high = DevicePolicy.random_init_high(seed=11)
+    low = DevicePolicy.random_init(seed=9)
+    envs = [HierVecEnv(n, seed=4) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        for rnd in range(3):
+            hier_rollout(e, high, low, 16, explore=True, step0=rnd * 16, trajectories=False)
+    mixed = done_seen = 0
+    for rnd in range(40 // k if k < 20 else 3):
+        step0 = 100 + rnd * k
+        tu = hier_rollout(envs[1], high, low, k, explore=True, step0=step0)
+        tf = hier_rollout(envs[0], high, low, k, explore=True, step0=step0, fused=True)
+        for f in ("acted", "agents", "rew_high", "rew_low", "done"):
+            assert torch.equal(tf[f], tu[f]), f
+        hi = tu["acted"] == N.HUM_AGENT_HIGH
+        lo = tu["acted"] == N.HUM_AGENT_LOW
+        for f, m in (("obs_high", hi), ("act_high", hi), ("obs_low", lo), ("act_low", lo)):
+            torch.testing.assert_close(tf[f][m], tu[f][m], atol=0, rtol=0, msg=f)
+        w = tu["acted"][:, : n // 4 * 4].view(k, -1, 4)
+        mixed += int(((w == N.HUM_AGENT_HIGH).any(-1) & (w == N.HUM_AGENT_LOW).any(-1)).sum())
+        done_seen += int(tu["done"].sum())
+        for name in ("obs_high", "obs", "done", "agents", "reward_high", "reward"):
+            torch.testing.assert_close(getattr(envs[0], name), getattr(envs[1], name), atol=0, rtol=0, msg=name)
+        m = envs[1].done.bool()
+        torch.testing.assert_close(envs[0].obs_high_reset[m], envs[1].obs_high_reset[m], atol=0, rtol=0)
+        torch.testing.assert_close(envs[0]._act_high_buf[hi[-1]], envs[1]._act_high_buf[hi[-1]], atol=0, rtol=0)
+        torch.testing.assert_close(envs[0]._act_low_buf[lo[-1]], envs[1]._act_low_buf[lo[-1]], atol=0, rtol=0)
+        p0, b0 = envs[0].get_state()
+        p1, b1 = envs[1].get_state()
+        np.testing.assert_array_equal(p0, p1)
+        np.testing.assert_array_equal(b0, b1)
+    print("fused hier rollout: %d mixed wave-transitions, %d dones" % (mixed, done_seen))
+    assert mixed > 0, "no wave held envs expecting different agents: the two-network path did not run"
+    assert done_seen > 0, "no auto-reset inside the compared rollouts"
+    for x in envs:
+        assert x.error_flags() == 0
+        x.close()
+    high.close()
+    low.close()
+
+
+def test_hier_rollout_fused_rejects_other_kernels():
+    high = DevicePolicy.random_init_high(seed=1)
+    low = DevicePolicy.random_init(seed=1)
+    env = HierVecEnv(64, seed=1, precision="fp64")
+    env.reset()
+    with pytest.raises(N.NativeError, match="hum_hier_rollout_fused"):
+        hier_rollout(env, high, low, 2, fused=True)
+    env.close()
+    high.close()
+    low.close()
+
+
 def test_hier_rollout_rejects_wrong_shapes():
     env = HierVecEnv(64, seed=1)
     env.reset()
