@@ -627,7 +627,13 @@ __device__ inline void nonfinite_outputs(const KArgs& a, long io, int frame, flo
             HUM_LDS float* orow = (HUM_LDS float*)obs_dst;
             for (int k = 0; k < HUM_NOBS; k++) orow[k] = 0.f;
         } else {
-            HUM_GLOBAL float* orow = (HUM_GLOBAL float*)(a.obs + io * HUM_NOBS);
+            long ro = io;
+#ifdef HUM_BOUNDS_CHECK
+            unsigned bf = 0;
+            HUM_BOUNDS(bf, ro >= 0 && ro < (long)a.ksteps * a.n, ro = 0);
+            if (bf) atomicOr(a.eflags, bf);
+#endif
+            HUM_GLOBAL float* orow = (HUM_GLOBAL float*)(a.obs + ro * HUM_NOBS);
             for (int k = 0; k < HUM_NOBS; k++) orow[k] = 0.f;
         }
     } else {
@@ -993,6 +999,10 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             group_substep<T, EPB_, TERRAIN>(a.P, sh, ge, (T*)a.scratch + (long)blockIdx.x * grow_block_size(EPB_, a.P.lds_rows),
                                    l, ef, tkey, frozen);
     }
+#ifdef HUM_SKIP_POST   // lane-utilisation study (tools/lane_util.py): the physics alone, no env logic / outputs
+    __syncthreads();
+    continue;
+#endif
     // hinge sin / cos of the final physics state, one dof per lane, for calc_state's kinematics on lane 0
     T* scs = &sh[ge].x.aba.IA[0][0];
     for (int d = l; d < NDOF; d += GL) {

@@ -354,6 +354,15 @@ __device__ inline void load_tab_lds() {   // block-wide; the caller's __syncthre
 #define HUM_MAXR_LDS 30
 #endif
 
+// Bounds-checked diagnostic build (-DHUM_BOUNDS_CHECK, csrc/Makefile target `bounds`; never the shipped library):
+// the sites that were generic-pointer (flat) accesses until round 4 check their index against
+// its slice; an index outside sets HUM_EFLAG_DIAG_BOUNDS and is clamped to the slice's first entry
+#ifdef HUM_BOUNDS_CHECK
+#define HUM_BOUNDS(ef, ok, fix) do { if (!(ok)) { (ef) |= HUM_EFLAG_DIAG_BOUNDS; fix; } } while (0)
+#else
+#define HUM_BOUNDS(ef, ok, fix) do {} while (0)
+#endif
+
 constexpr int MAXR_LDS = HUM_MAXR_LDS;
 
 template <typename T>
@@ -471,6 +480,18 @@ static __shared__ unsigned long long s_tlast;   // shared: markers also sit insi
 #else
 #define PHASE(k) do { } while (0)
 #define PHASE_INIT do { } while (0)
+#endif
+
+// Lane-utilisation study (tools/lane_util.py; diagnostic builds only): -DHUM_STOP_AFTER=k ends every substep after
+// phase k (0 = before FK; 9 = the whole substep), so SQ counters of builds k - 1 and k, stepped from the same saved
+// states, differ by phase k's instructions and thread-cycles
+#ifdef HUM_STOP_AFTER
+#define HUM_STOP(k)                                                              \
+    do {                                                                         \
+        if constexpr (HUM_STOP_AFTER == (k)) return;                             \
+    } while (0)
+#else
+#define HUM_STOP(k) do { } while (0)
 #endif
 
 #if defined(HUM_WAVE_LOG) && defined(HUM_SUBPHASE)   // finer split of a phase's time (tools/wave_log.py)
@@ -780,7 +801,7 @@ constexpr bool delassus_kernel() { return DELASSUS_ON && sizeof(T) == 4 && EPB_ 
 
 template <typename T, int EPB_>
 __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, GroupLDS<T>* shb, T* gblock, int nl, int nc,
-                                                          const T dt, int& pbase, int& ptot, bool& lam) {
+                                                          const T dt, int& pbase, int& ptot, bool& lam, unsigned& ef) {
     const ModelTab<T>& M = tab_fresh<T>();
     const int lane = threadIdx.x & 63, cap = P.lds_rows;
     const T idt = T(1) / dt;
@@ -847,7 +868,9 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
 #pragma unroll
                 for (int k = 0; k < CW; k++) ce[k] = lc[k];
             } else {
-                const HUM_GLOBAL T* gc = (const HUM_GLOBAL T*)(gblock + gcon_offset(EPB_, cap, e) + (long)(cidx - MAXC_LDS) * CW);
+                int ci = cidx - MAXC_LDS, ce_env = e;   // the env's spill slice: MAXC_G - MAXC_LDS contacts
+                HUM_BOUNDS(ef, ci >= 0 && ci < MAXC_G - MAXC_LDS && ce_env >= 0 && ce_env < EPB_, (ci = 0, ce_env = 0));
+                const HUM_GLOBAL T* gc = (const HUM_GLOBAL T*)(gblock + gcon_offset(EPB_, cap, ce_env) + (long)ci * CW);
 #pragma unroll
                 for (int k = 0; k < CW; k++) ce[k] = __builtin_nontemporal_load(gc + k);
             }
@@ -1493,6 +1516,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     const ModelTab<T>& M = tab_fresh<T>();
     const T dt = (T)P.dt;
     PHASE_INIT;
+    HUM_STOP(0);
     // ---- FK (every lane, registers); lane 0 publishes
     {
         // the 17 hinge angles' sin / cos once, one per lane (scratch: the ABA transients are dead until pass 1)
@@ -1539,6 +1563,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     phase_sync();
     PHASE(1);
+    HUM_STOP(1);
     // ---- ABA pass 1: lane b = body b
     if (l < NB) {
         const int b = l;
@@ -1656,6 +1681,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     phase_sync();
     PHASE(2);
+    HUM_STOP(2);
     // ---- ABA pass 2 (leaves -> root) by tree level: 4 steps {shins, lower arms} -> {thighs, upper arms}
     //      -> pelvis -> lwaist instead of 10 sequential bodies.  In a step, lane group g (4 lanes) updates
     //      one body redundantly in registers (dof count padded to 3 with identity pivots, so every body runs
@@ -1678,6 +1704,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     phase_sync();
     PHASE(3);
+    HUM_STOP(3);
     // ---- base + pass 3 (redundant on every lane); lane 0 publishes L0 and nu* = clamp(nu + dt acc)
     {
         // base (redundant on every lane), then the forward pass by tree level (root -> leaves, one body per
@@ -1727,6 +1754,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     phase_sync();
     PHASE(4);
+    HUM_STOP(4);
     // ---- geom endpoints (lane g; lane 0 also the 17th) and joint-limit scan
     auto& C = S.x.cr;
     // per-geom table for the contact phase, in the row storage the rows phase has not written yet (the survivor
@@ -1775,6 +1803,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     }
     phase_sync();
     PHASE(5);
+    HUM_STOP(5);
     // ---- contacts, compacted in candidate order (ground points, then geom pairs)
     const int maxc = P.max_contacts < MAXC_G ? P.max_contacts : MAXC_G;
     int nc = 0, over = 0;
@@ -1924,16 +1953,18 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
     if (over) ef |= HUM_EFLAG_CONTACT_OVERFLOW;
     __syncthreads();
     PHASE(6);
+    HUM_STOP(6);
     // ---- rows (limits, normals, frictions): Jacobian + test-impulse response, one row per lane, the rows of
     //      all EPB_ envs of the wave spread over its lanes (one round instead of max_e ceil(nrows_e / 16))
     const int nrows = nl + 3 * nc;
     int pbase, ptot;   // this env's first pool position, the block's pool positions in use
     bool lam;          // the Delassus-form PGS (wave-uniform)
-    group_rows<T, EPB_>(P, shb, gblock, nl, nc, dt, pbase, ptot, lam);
+    group_rows<T, EPB_>(P, shb, gblock, nl, nc, dt, pbase, ptot, lam, ef);
     const int cap = P.lds_rows;
     WLOG(1, env_max<EPB_>(nrows));
     __syncthreads();
     PHASE(7);
+    HUM_STOP(7);
     // ---- PGS (lane l owns nu[l] and nu[16+l]).  Every lane recomputes lambda identically and only
     //      re-reads values it wrote itself, so no cross-lane LDS ordering is needed inside the loop.
     T n0 = S.nu[l], n1 = l < NV - GL ? S.nu[GL + l] : T(0);
@@ -2103,10 +2134,12 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         // access is an LDS or a global one chosen per value, never one through a generic pointer that may point at
         // either (a flat access)
         auto rd = [&](int p, int w) -> T {
+            HUM_BOUNDS(ef, p >= 0 && p < EPB_ * MAXR_G, p = 0);   // the LDS pool, then the block's spill rows
             if (p < cap) return ((const HUM_LDS T*)((const HUM_LDS char*)shb + pool_off<T>(p)))[w];
             return __builtin_nontemporal_load((const HUM_GLOBAL T*)(gblock + (long)(p - cap) * RW) + w);
         };
         auto wr = [&](int p, int w, T v) {
+            HUM_BOUNDS(ef, p >= 0 && p < EPB_ * MAXR_G, p = 0);
             if (p < cap) ((HUM_LDS T*)((HUM_LDS char*)shb + pool_off<T>(p)))[w] = v;
             else __builtin_nontemporal_store(v, (HUM_GLOBAL T*)(gblock + (long)(p - cap) * RW) + w);
         };
@@ -2132,6 +2165,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             for (int r = 0; r < nrows; r++) solve(pbase + pool_pos(r, nl, nc), r);
     }
     PHASE(8);
+    HUM_STOP(8);
     S.nu[l] = n0;
     if (l < NV - GL) S.nu[GL + l] = n1;
     // ---- integrate (lanes split the state), lane 0 the quaternion.  A frozen env (no action this round, a

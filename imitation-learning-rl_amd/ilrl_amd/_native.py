@@ -23,6 +23,7 @@ HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
 HUM_STEP_AUTORESET, HUM_STEP_SKIP_PHYSICS, HUM_STEP_HOST_IO, HUM_STEP_CHECK_FINITE = 1, 2, 4, 8
 HUM_MODE_DEBUG, HUM_MODE_PREDEFINED = 1, 2
 HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW, HUM_EFLAG_BAD_START_FRAME = 1, 2, 4, 8
+HUM_EFLAG_DIAG_BOUNDS = 0x80000000   # bounds-checked diagnostic builds only (-DHUM_BOUNDS_CHECK)
 HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
 HUM_RESET_NO_REF_POSE, HUM_RESET_NO_INIT_VEL = 1, 2
 HUM_MAX_CONTACTS = 95

@@ -81,6 +81,8 @@ extern "C" {
 #define HUM_EFLAG_CONTACT_OVERFLOW 4u   /* more contacts than a lowered max_contacts (never with the default) */
 #define HUM_EFLAG_BAD_START_FRAME 8u    /* resetFromFrame start frame past the clip (the reference's iloc raises
                                            IndexError): lane left unchanged */
+#define HUM_EFLAG_DIAG_BOUNDS 0x80000000u  /* bounds-checked diagnostic builds only (-DHUM_BOUNDS_CHECK): an index left
+                                         its slice at a former generic-pointer access site (clamped) */
 
 /* bookkeeping layout (doubles; integers stored exactly) */
 enum {
