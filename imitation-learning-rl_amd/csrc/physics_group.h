@@ -1506,6 +1506,113 @@ __device__ __attribute__((always_inline)) void group_fwd_level(const PhysParams&
 
 // ------------------------------------------------------------------------- one cooperative substep
 // Called by all 64 lanes of the block (uniform control flow at every __syncthreads).
+// ---- FK by root-to-leaf chains.  The tree (torso; lwaist - pelvis - thigh - shin twice; upper - lower arm twice) is
+// four chains of at most four bodies: {1 2 3 4}, {7 8}, {9 10}, {1 2 5 6} (the fourth repeats lwaist and pelvis rather
+// than waiting for them).  Lane l of an env is chain l >> 2, frame row l & 3 (row 3 idle): a row of a body's frame
+// depends only on the same row of its parent's frame (M = R_p Roff, o = o_p + R_p toff, and the hinge rotations mix
+// columns within a row), so 12 lanes walk the four chains in four dependent steps instead of lane 0 composing all ten
+// bodies.  Every value is formed by the same operations as forward_kinematics_pre (zero constants skipped, the same
+// contracted expressions): the frames are bit-identical.  At a chain depth every chain's body has the same dof count;
+// the per-lane constants are selects among the four chains' compile-time values.  Opt-in (-DHUM_FK_CHAIN): bitwise
+// equal to the serial FK but 1.9 % slower same-box (35.84 vs 36.54 M env-steps/s; wave log FK 19.1 K -> 26.8 K cycles
+// per block-step, profiles/r05_fk_chain_ab.txt): the selects and zero-skip compares triple the FK's VALU instructions,
+// and at one wave per SIMD a VALU instruction costs its issue slot whatever its exec mask.
+constexpr int FK_CH[4][4] = {{1, 2, 3, 4}, {7, 8, -1, -1}, {9, 10, -1, -1}, {1, 2, 5, 6}};
+constexpr double fk_roff(int dd, int ch, int k) { return FK_CH[ch][dd] < 0 ? 0.0 : body_Roff[9 * FK_CH[ch][dd] + k]; }
+constexpr double fk_toff(int dd, int ch, int k) { return FK_CH[ch][dd] < 0 ? 0.0 : body_toff[3 * FK_CH[ch][dd] + k]; }
+constexpr int fk_body(int dd, int ch) { return FK_CH[ch][dd]; }
+constexpr int fk_dof(int dd, int ch, int k) { return FK_CH[ch][dd] < 0 ? 0 : body_dof0[FK_CH[ch][dd]] + k; }
+constexpr int fk_ndof(int dd) { return body_ndof[FK_CH[0][dd]]; }
+constexpr bool fk_uniform_axis(int dd, int k) {
+    for (int c = 1; c < 4; c++)
+        if (FK_CH[c][dd] >= 0 && dof_axis[fk_dof(dd, c, k)] != dof_axis[fk_dof(dd, 0, k)]) return false;
+    return true;
+}
+constexpr bool fk_check() {   // same dof count across the chains at each depth
+    for (int dd = 0; dd < 4; dd++)
+        for (int c = 0; c < 4; c++)
+            if (FK_CH[c][dd] >= 0 && body_ndof[FK_CH[c][dd]] != fk_ndof(dd)) return false;
+    return true;
+}
+static_assert(NB == 11 && fk_check(), "FK chains: the humanoid tree of model_gen.h");
+template <typename T>
+__device__ __attribute__((always_inline)) inline T fk_sel(int ch, double v0, double v1, double v2, double v3) {
+    return ch == 0 ? (T)v0 : (ch == 1 ? (T)v1 : (ch == 2 ? (T)v2 : (T)v3));
+}
+__device__ __attribute__((always_inline)) inline int fk_seli(int ch, int v0, int v1, int v2, int v3) {
+    return ch == 0 ? v0 : (ch == 1 ? v1 : (ch == 2 ? v2 : v3));
+}
+// one row of rot_post (physics.h): the same expressions, the axis per lane
+template <typename T>
+__device__ __attribute__((always_inline)) inline void fk_rot_row(T* m, int ax, T c, T s) {
+#pragma clang fp contract(on)   // per-expression fusion only, as rot_post
+    const T mi = ax == 0 ? m[1] : (ax == 1 ? m[2] : m[0]);   // column (ax + 1) % 3
+    const T mj = ax == 0 ? m[2] : (ax == 1 ? m[0] : m[1]);   // column (ax + 2) % 3
+    const T ni = c * mi + s * mj;
+    const T nj = -s * mi + c * mj;
+    m[0] = ax == 0 ? m[0] : (ax == 1 ? nj : ni);
+    m[1] = ax == 0 ? ni : (ax == 1 ? m[1] : nj);
+    m[2] = ax == 0 ? nj : (ax == 1 ? ni : m[2]);
+}
+template <typename T, int AX>
+__device__ __attribute__((always_inline)) inline void fk_rot_row_c(T* m, T c, T s) {
+#pragma clang fp contract(on)
+    constexpr int i = (AX + 1) % 3, j = (AX + 2) % 3;
+    const T mi = m[i], mj = m[j];
+    m[i] = c * mi + s * mj;
+    m[j] = -s * mi + c * mj;
+}
+// chain depth DD for lane (ch, row): Rp / op = the parent's frame row in, the body's out; publishes it
+template <typename T, int DD>
+__device__ __attribute__((always_inline)) inline void fk_depth(GroupLDS<T>& S, const T* scs, int ch, int row, T* Rp, T& op) {
+#pragma clang fp contract(on)
+    const int b = fk_seli(ch, fk_body(DD, 0), fk_body(DD, 1), fk_body(DD, 2), fk_body(DD, 3));
+    if (b < 0) return;
+    T M[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {   // (R_p Roff)[row][c] as forward_kinematics_pre forms it
+        const T c0 = fk_sel<T>(ch, fk_roff(DD, 0, c), fk_roff(DD, 1, c), fk_roff(DD, 2, c), fk_roff(DD, 3, c));
+        const T c1 = fk_sel<T>(ch, fk_roff(DD, 0, 3 + c), fk_roff(DD, 1, 3 + c), fk_roff(DD, 2, 3 + c), fk_roff(DD, 3, 3 + c));
+        const T c2 = fk_sel<T>(ch, fk_roff(DD, 0, 6 + c), fk_roff(DD, 1, 6 + c), fk_roff(DD, 2, 6 + c), fk_roff(DD, 3, 6 + c));
+        T m = c0 == T(0) ? T(-0.0) : Rp[0] * c0;
+        m = c1 == T(0) ? m : fma(Rp[1], c1, m);
+        M[c] = c2 == T(0) ? m : fma(Rp[2], c2, m);
+    }
+    {
+        const T t0 = fk_sel<T>(ch, fk_toff(DD, 0, 0), fk_toff(DD, 1, 0), fk_toff(DD, 2, 0), fk_toff(DD, 3, 0));
+        const T t1 = fk_sel<T>(ch, fk_toff(DD, 0, 1), fk_toff(DD, 1, 1), fk_toff(DD, 2, 1), fk_toff(DD, 3, 1));
+        const T t2 = fk_sel<T>(ch, fk_toff(DD, 0, 2), fk_toff(DD, 1, 2), fk_toff(DD, 2, 2), fk_toff(DD, 3, 2));
+        T o = t0 == T(0) ? op : fma(Rp[0], t0, op);
+        o = t1 == T(0) ? o : fma(Rp[1], t1, o);
+        op = t2 == T(0) ? o : fma(Rp[2], t2, o);
+    }
+    const bool pub = ch != 3 || DD >= 2;   // chain 3 repeats lwaist and pelvis, which chain 0 publishes
+    static_for<fk_ndof(DD)>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int d = fk_seli(ch, fk_dof(DD, 0, k), fk_dof(DD, 1, k), fk_dof(DD, 2, k), fk_dof(DD, 3, k));
+        const T sg = fk_sel<T>(ch, dof_sign[fk_dof(DD, 0, k)], dof_sign[fk_dof(DD, 1, k)], dof_sign[fk_dof(DD, 2, k)],
+                               dof_sign[fk_dof(DD, 3, k)]);
+        const T cs = scs[2 * d + 1], sn = sg * scs[2 * d];
+        if constexpr (fk_uniform_axis(DD, k)) {
+            constexpr int AX = dof_axis[fk_dof(DD, 0, k)];
+            if (pub) S.Sc[d][row] = M[AX] * sg;
+            fk_rot_row_c<T, AX>(M, cs, sn);
+        } else {
+            const int ax = fk_seli(ch, dof_axis[fk_dof(DD, 0, k)], dof_axis[fk_dof(DD, 1, k)], dof_axis[fk_dof(DD, 2, k)],
+                                   dof_axis[fk_dof(DD, 3, k)]);
+            if (pub) S.Sc[d][row] = (ax == 0 ? M[0] : (ax == 1 ? M[1] : M[2])) * sg;
+            fk_rot_row(M, ax, cs, sn);
+        }
+    });
+    if (pub) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) S.R[b][3 * row + c] = M[c];
+        S.o[b][row] = op;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) Rp[c] = M[c];
+}
+
 template <typename T, int EPB_, bool TERRAIN = false>   // TERRAIN: heightfield ground (hum_set_terrain)
 __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P, GroupLDS<T>* shb, const int ge,
                                                              T* gblock, const int l, unsigned& ef,
@@ -1532,6 +1639,7 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
         T quat[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) quat[e] = S.st[3 + e];
+#ifndef HUM_FK_CHAIN   // lane 0 composes every body (forward_kinematics_pre) and publishes
         Kin<T> K;
         forward_kinematics_pre(quat, scs, K);
         SUBPHASE(12);
@@ -1548,6 +1656,28 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
 #pragma unroll
                 for (int i = 0; i < 3; i++) S.Sc[d][i] = K.u[d][i];
         }
+#else
+        {   // -DHUM_FK_CHAIN (measured slower): lane (chain l >> 2, row l & 3) walks a chain
+            const int ch = l >> 2, row = l & 3;
+            if (row < 3) {
+                T R0[9];
+                quat_to_mat(quat, R0);
+                T Rp[3], op = T(0);
+#pragma unroll
+                for (int c = 0; c < 3; c++) Rp[c] = row == 0 ? R0[c] : (row == 1 ? R0[3 + c] : R0[6 + c]);
+                if (ch == 0) {
+#pragma unroll
+                    for (int c = 0; c < 3; c++) S.R[0][3 * row + c] = Rp[c];
+                    S.o[0][row] = T(0);
+                }
+                fk_depth<T, 0>(S, scs, ch, row, Rp, op);
+                fk_depth<T, 1>(S, scs, ch, row, Rp, op);
+                fk_depth<T, 2>(S, scs, ch, row, Rp, op);
+                fk_depth<T, 3>(S, scs, ch, row, Rp, op);
+            }
+        }
+        SUBPHASE(12);
+#endif
         if (l < 16) {   // generalised velocity
             S.nu[l] = l < 3 ? S.st[10 + l] : (l < 6 ? S.st[7 + l - 3] : S.st[30 + l - 6]);
             if (l < NV - 16) S.nu[16 + l] = S.st[30 + 10 + l];

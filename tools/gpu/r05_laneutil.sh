@@ -14,4 +14,4 @@ for v in ${VARIANTS:-lu0 lu1 lu2 lu3 lu4 lu5 lu6 lu7 lu8 lu9 luall}; do
   tail -1 $O/$v.log
 done
 rm -f $O/state.npz
-python3 tools/lane_util.py summary $O | tee $O/summary.txt
+python3 tools/lane_util.py dump $O && python3 tools/lane_util.py summary $O | tee $O/summary.txt

@@ -3,7 +3,8 @@
 usage: lane_util.py save OUT.npz    (default library: 4096 lanes x motion02_04, 200 random-action env steps in
                                      launches of k = 32 from a reset, then the physics state + bookkeeping saved)
        lane_util.py run STATE.npz   (ILRL_AMD_LIB = a variant: 4 single-step launches, each from the saved state)
-       lane_util.py summary DIR     (DIR/<variant>/run_results.db from rocprofv3 --pmc: the per-phase table)
+       lane_util.py dump DIR        (DIR/<variant>/**/run_results.db from rocprofv3 --pmc -> DIR/<variant>.json)
+       lane_util.py summary DIR     (the per-phase table from DIR/calib.json and DIR/lu*.json)
 
 Variants (tools/build_variant.sh): lu0 .. lu8 = group_f32.hip with -DHUM_STOP_AFTER=k (every substep ends after
 phase k), lu9 = the whole substep without the env logic (-DHUM_SKIP_POST), luall = the full kernel.  Phase k's counts
@@ -62,11 +63,27 @@ def counters(db, kp):
     return out
 
 
+def dump(d):
+    """DIR/<variant>/**/run_results.db -> DIR/<variant>.json (the counters this study reads; the database goes)."""
+    import json
+    import shutil
+    for sub in sorted(glob.glob(os.path.join(d, "*", ""))):
+        name = os.path.basename(os.path.dirname(sub))
+        dbs = glob.glob(os.path.join(sub, "**", "*results.db"), recursive=True)
+        if not dbs:
+            continue
+        if name == "calib":
+            out = {str(m): counters(dbs[0], "lanes_active<%d>" % m) or counters(dbs[0], "lanes_activeILi%dE" % m)
+                   for m in (64, 32, 16, 4, 1)}
+        else:
+            out = counters(dbs[0], "step_group_kernel")
+        json.dump(out, open(os.path.join(d, name + ".json"), "w"), indent=1)
+        shutil.rmtree(sub)
+
+
 def summary(d):
-    cal = {}
-    for db in glob.glob(os.path.join(d, "calib", "**", "*results.db"), recursive=True):
-        for m in (64, 32, 16, 4, 1):
-            cal[m] = counters(db, "lanes_active<%d>" % m) or counters(db, "lanes_activeILi%dE" % m)
+    import json
+    cal = {int(m): c for m, c in json.load(open(os.path.join(d, "calib.json"))).items()}
     lines = ["# VALU counter calibration (tools/micro/lane_util.hip, 1024 waves x 16384 fma per active lane)",
              "# M active lanes: INSTS_VALU/wave, ACTIVE_INST_VALU/wave (quad-cycles), THREAD_CYCLES_VALU/wave, "
              "THREAD_CYCLES / INSTS"]
@@ -77,16 +94,15 @@ def summary(d):
             continue
         w = c.get("SQ_WAVES", 1024) or 1024
         ratio = c["SQ_THREAD_CYCLES_VALU"] / c["SQ_INSTS_VALU"]
-        lines.append("  M=%2d  insts %.0f  active %.0f  thread_cycles %.0f  thread_cycles/inst %.2f" % (
-            m, c["SQ_INSTS_VALU"] / w, c["SQ_ACTIVE_INST_VALU"] / w, c["SQ_THREAD_CYCLES_VALU"] / w, ratio))
+        lines.append("  M=%2d  insts %.0f  active %.0f  thread_cycles %.0f  thread_cycles/inst %.2f  FP32 FLOP/wave %.0f" % (
+            m, c["SQ_INSTS_VALU"] / w, c["SQ_ACTIVE_INST_VALU"] / w, c["SQ_THREAD_CYCLES_VALU"] / w, ratio,
+            c.get("SQ_INSTS_VALU_FLOPS_FP32", 0) / w))
         if m == 64:
             tc_per_lane_inst = ratio / 64
-    var = {}
-    for db in glob.glob(os.path.join(d, "lu*", "**", "*results.db"), recursive=True):
-        name = os.path.relpath(db, d).split(os.sep)[0]
-        var[name] = counters(db, "step_group_kernel")
+    var = {os.path.basename(f)[:-5]: json.load(open(f)) for f in glob.glob(os.path.join(d, "lu*.json"))}
     lines.append("# per launch of 4096 lanes (1024 waves), one env step; phase k = variant k - variant k-1")
-    lines.append("%-46s %12s %8s %14s %8s %10s" % ("phase", "VALU insts", "/wave", "thread-cycles", "lanes", "FP32 FLOP"))
+    lines.append("%-46s %12s %8s %14s %8s %10s %10s" % ("phase", "VALU insts", "/wave", "thread-cycles", "lanes",
+                                                          "FP32 FLOP", "cyc/wave"))
     prev = None
     rows = []
     order = ["lu%d" % k for k in range(10)] + ["luall"]
@@ -103,7 +119,8 @@ def summary(d):
         insts, tcyc, flops, waves = dlt[0], dlt[1], dlt[3], c.get("SQ_WAVES", 1024) or 1024
         lanes = tcyc / (insts * tc_per_lane_inst) if insts > 0 and tc_per_lane_inst else float("nan")
         rows.append((lab, insts, tcyc, lanes, flops))
-        lines.append("%-46s %12.0f %8.0f %14.0f %8.1f %10.0f" % (lab, insts, insts / waves, tcyc, lanes, flops))
+        lines.append("%-46s %12.0f %8.0f %14.0f %8.1f %10.0f %10.0f" % (lab, insts, insts / waves, tcyc, lanes, flops,
+                                                                      4 * dlt[7] / waves))
     if "luall" in var:
         c = var["luall"]
         tot_i, tot_t = c["SQ_INSTS_VALU"], c["SQ_THREAD_CYCLES_VALU"]
@@ -114,4 +131,4 @@ def summary(d):
 
 
 if __name__ == "__main__":
-    {"save": save, "run": run, "summary": summary}[sys.argv[1]](sys.argv[2])
+    {"save": save, "run": run, "dump": dump, "summary": summary}[sys.argv[1]](sys.argv[2])
