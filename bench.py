@@ -263,8 +263,14 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
                 pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s + soff[0], out=actbuf)
                 return env.step(actbuf, autoreset=True)
             if a.fused:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
+                traj_out = {}   # by launch size, reused launch to launch
+
                 def step(s, kk=k):
-                    return pol.rollout(env, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True, fused=True)
+                    o = traj_out.get(kk)
+                    tr = pol.rollout(env, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True, fused=True,
+                                     out=o)
+                    traj_out.setdefault(kk, tr)
+                    return tr
     env.reset()
     env.done.zero_()
     for w in range(wlaunches):
@@ -285,6 +291,12 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     if a.hier and a.policy:   # the timed launches' trajectory buffers
         for s, kk in enumerate(sizes):
             traj_bufs(kk, s)
+    elif a.policy and a.fused:
+        for kk in set(sizes):
+            if kk not in traj_out:
+                traj_out[kk] = {"obs": torch.empty(kk, n, 70, device=dev), "actions": torch.empty(kk, n, 17, device=dev),
+                                "rewards": torch.empty(kk, n, device=dev),
+                                "dones": torch.empty(kk, n, dtype=torch.uint8, device=dev)}
     if not a.policy:
         # every output buffer the timed launches write exists before the clock starts (a warmup shorter than k, e.g.
         # the driver's --steps 20 --warmup 5, never ran a launch of the timed shape: its allocation and zero fill

@@ -118,22 +118,29 @@ class DevicePolicy:
                 "hum_policy_act")
         return act
 
-    def rollout(self, venv, k, explore=True, step0=0, trajectories=True, fused=False):
+    def rollout(self, venv, k, explore=True, step0=0, trajectories=True, fused=False, out=None):
         """k sampler steps (policy -> env step with auto-reset) on venv's lanes, all on the device with no host
         round trip.  venv.obs must hold the current observation (after venv.reset()).  Returns the trajectory
         tensors {obs [k,n,70] (policy inputs), actions [k,n,17] (the samples before clip_actions, as RLlib records
         them), rewards [k,n], dones [k,n]} (or {}).  fused: one launch with the policy inside the step kernel
-        (hum_rollout_fused; cooperative fp32 handles with 4 envs per block on the plane)."""
+        (hum_rollout_fused; cooperative fp32 handles with 4 envs per block on the plane).  out: a dict of the same
+        tensors to write into (reused across calls, e.g. by a timed loop) instead of fresh ones."""
         t = self.torch
         n = venv.n
         if not hasattr(venv, "_act_buf"):
             venv._act_buf = t.zeros(n, N.HUM_NACT, dtype=t.float32, device=venv.device)
         tr = {}
         if trajectories:
-            tr = {"obs": t.empty(k, n, N.HUM_NOBS, dtype=t.float32, device=venv.device),
-                  "actions": t.empty(k, n, N.HUM_NACT, dtype=t.float32, device=venv.device),
-                  "rewards": t.empty(k, n, dtype=t.float32, device=venv.device),
-                  "dones": t.empty(k, n, dtype=t.uint8, device=venv.device)}
+            shapes = {"obs": ((N.HUM_NOBS,), t.float32), "actions": ((N.HUM_NACT,), t.float32),
+                      "rewards": ((), t.float32), "dones": ((), t.uint8)}
+            for f, (sh, dt) in shapes.items():
+                x = out.get(f) if out else None
+                if x is None:
+                    x = t.empty((k, n) + sh, dtype=dt, device=venv.device)
+                elif tuple(x.shape) != (k, n) + sh or x.dtype != dt or x.device != venv.device or not x.is_contiguous():
+                    raise ValueError("rollout: out[%r] must be a contiguous %s tensor of shape %s on %s"
+                                     % (f, dt, (k, n) + sh, venv.device))
+                tr[f] = x
         p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
         fn = N.lib().hum_rollout_fused if fused else N.lib().hum_rollout
         N.check(fn(venv.h, self.h, k, int(bool(explore)), ctypes.c_uint64(step0), p(venv.obs),

@@ -268,6 +268,30 @@ def test_hier_rollout_fused_equals_hier_rollout(n, k):
     low.close()
 
 
+def test_hier_rollout_fused_without_trajectory():
+    """No trajectory rows: the per-transition agents / rewards / done go to the handle's scratch (grown on demand),
+    and the env buffers and the state still equal the per-transition loop's, call after call."""
+    n = 256
+    high = DevicePolicy.random_init_high(seed=3)
+    low = DevicePolicy.random_init(seed=5)
+    envs = [HierVecEnv(n, seed=8) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    for rnd, k in enumerate((8, 24, 8)):   # the scratch grows, then is reused
+        hier_rollout(envs[0], high, low, k, explore=True, step0=rnd * 32, trajectories=False, fused=True)
+        hier_rollout(envs[1], high, low, k, explore=True, step0=rnd * 32, trajectories=False)
+        for name in ("obs_high", "obs", "done", "agents", "reward_high", "reward"):
+            torch.testing.assert_close(getattr(envs[0], name), getattr(envs[1], name), atol=0, rtol=0, msg=name)
+        p0, b0 = envs[0].get_state()
+        p1, b1 = envs[1].get_state()
+        np.testing.assert_array_equal(p0, p1)
+        np.testing.assert_array_equal(b0, b1)
+    for x in envs:
+        x.close()
+    high.close()
+    low.close()
+
+
 def test_hier_rollout_fused_rejects_other_kernels():
     high = DevicePolicy.random_init_high(seed=1)
     low = DevicePolicy.random_init(seed=1)

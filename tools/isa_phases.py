@@ -30,7 +30,7 @@ def main():
                           + (HOTFLAGS if HOT else [])
                           + os.environ.get("ISA_FLAGS", "").split())
     lines = open(out).read().split("\n")
-    st = [i for i, l in enumerate(lines) if re.match(r"_ZN3hkk17step_group_kernelIfLi4ELb0ELb0EEEvNS_5KArgsE:", l)][0]
+    st = [i for i, l in enumerate(lines) if re.match(r"_ZN3hkk17step_group_kernelIfLi4ELb0EL[bi]0EEEvNS_5KArgsE:", l)][0]
     en = [i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end")][0]
     cur = 0
     cnt = collections.defaultdict(collections.Counter)
