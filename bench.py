@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--fused", action="store_true",
                     help="with --policy: one hum_rollout_fused launch per --k steps (the policy inside the env kernel) "
                          "instead of a policy launch + an env launch per step")
+    ap.add_argument("--sample-batch", action="store_true",
+                    help="with --fused --policy (or --hier --policy): after every rollout launch also form the policy "
+                         "columns RLlib's sampler records - action_dist_inputs, action_logp and vf_preds from a "
+                         "value branch of the same shape (random-init) - over the launch's rows")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / parity side measurements")
     return ap.parse_args()
 
@@ -238,9 +242,20 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
                 o["acted"] = acted.setdefault(s + soff[0], torch.empty(kk, n, dtype=torch.uint8, device=dev))
                 return o
 
+            vhigh = vlow = None
+            if a.sample_batch:
+                vhigh = DevicePolicy.random_init_value(seed=27 + rank, device=dev.index, n_in=44)
+                vlow = DevicePolicy.random_init_value(seed=37 + rank, device=dev.index)
+            cols_out = {}
+
             def step(s, kk=k):   # launch numbers (and the exploration noise's step index) continue past the warm-up
-                return hier_rollout(env, high, low, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True,
-                                    fused=a.fused, out=traj_bufs(kk, s))
+                tr = hier_rollout(env, high, low, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True,
+                                  fused=a.fused, out=traj_bufs(kk, s))
+                if a.sample_batch:   # both agents' columns over all rows (the acting agent's rows are the valid ones)
+                    ch, cl = cols_out.setdefault(kk, ({}, {}))
+                    ch.update(high.sample_batch_columns(tr["obs_high"], tr["act_high"], value=vhigh, out=ch))
+                    cl.update(low.sample_batch_columns(tr["obs_low"], tr["act_low"], value=vlow, out=cl))
+                return tr
             env._bench_acted = acted
     else:
         from ilrl_amd.clips import CLIP_NAMES
@@ -265,11 +280,17 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             if a.fused:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
                 traj_out = {}   # by launch size, reused launch to launch
 
+                vpol = DevicePolicy.random_init_value(seed=27 + rank, device=dev.index) if a.sample_batch else None
+                cols_out = {}
+
                 def step(s, kk=k):
                     o = traj_out.get(kk)
                     tr = pol.rollout(env, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True, fused=True,
                                      out=o)
                     traj_out.setdefault(kk, tr)
+                    if a.sample_batch:
+                        c = cols_out.setdefault(kk, {})
+                        c.update(pol.sample_batch_columns(tr["obs"], tr["actions"], value=vpol, out=c))
                     return tr
     env.reset()
     env.done.zero_()
@@ -464,6 +485,7 @@ def main():
                                         "hum_hier_rollout call (2 policy launches + 1 env launch per transition)")
                                        if a.hier and a.policy else "launch"),
                        "fused": bool(a.policy and a.fused),
+                       "sample_batch_columns": bool(a.policy and a.sample_batch),
                        "envs_per_gpu": n, "clip": a.clip, "k": a.k,
                        # the launches the timed region actually ran (--steps < k: one shorter launch)
                        "launches": len(sizes), "steps_per_launch": max(sizes),

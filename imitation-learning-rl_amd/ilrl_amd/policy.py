@@ -90,6 +90,69 @@ class DevicePolicy:
         w["log_std"] = w["log_std"].reshape(-1)
         return cls(w, device=device, seed=seed, n_in=n_in, n_out=n_out)
 
+    @classmethod
+    def value_from_rllib_weights(cls, weights, device=0, n_in=N.HUM_NOBS):
+        """The value branch of the same TF FullyConnectedNetwork (RLlib 1.2 PPO: vf_share_layers False, so
+        fc_value_1 -> fc_value_2 -> value_out, tanh, the same hidden sizes) as a 1-output network: act(...,
+        mean_out=v) gives the value predictions (SampleBatch VF_PREDS).  Name mapping as from_rllib_weights."""
+        def pick(sub):
+            hits = [k for k in weights if sub in k]
+            if len(hits) != 1:
+                raise KeyError("expected exactly one variable matching %r, got %s" % (sub, hits))
+            return np.asarray(weights[hits[0]])
+        w = {"w1": pick("fc_value_1/kernel"), "b1": pick("fc_value_1/bias"), "w2": pick("fc_value_2/kernel"),
+             "b2": pick("fc_value_2/bias"), "w3": pick("value_out/kernel"), "b3": pick("value_out/bias")}
+        return cls(w, device=device, n_in=n_in, n_out=1)
+
+    @classmethod
+    def random_init_value(cls, seed=0, device=0, n_in=N.HUM_NOBS):
+        """A value branch with RLlib's initialisers (normc 1.0 hidden, 0.01 output), for benchmarks and tests."""
+        rng = np.random.default_rng(seed)
+        w = {"w1": _normc(rng, (n_in, H), 1.0), "b1": np.zeros(H), "w2": _normc(rng, (H, H), 1.0), "b2": np.zeros(H),
+             "w3": _normc(rng, (H, 1), 0.01), "b3": np.zeros(1)}
+        return cls(w, device=device, seed=seed, n_in=n_in, n_out=1)
+
+    def sample_batch_columns(self, obs, actions, value=None, out=None):
+        """The policy-side SampleBatch columns RLlib's sampler records per step, for recorded policy inputs obs
+        [..., n_in] and raw samples actions [..., n_out] (device; e.g. a rollout's trajectory, any leading shape):
+        action_dist_inputs [..., 2 n_out] (the DiagGaussian's mean and log_std), action_logp [...] (log-density of
+        the raw sample) and, given the value branch `value` (a 1-output DevicePolicy), vf_preds [...].  One
+        policy launch (and one value launch) over all rows: within a fragment the weights are fixed, so this equals
+        what the per-step compute_actions records.  out: a dict of the same tensors to write into."""
+        t = self.torch
+        lead = tuple(obs.shape[:-1])
+        R = int(np.prod(lead)) if lead else 1
+        o2 = obs.reshape(R, self.n_in)
+        out = out if out is not None else {}
+        mean = t.empty(R, self.n_out, dtype=t.float32, device=self.device)
+        scratch = t.empty(R, self.n_out, dtype=t.float32, device=self.device)   # the clipped actions (unused)
+        self.act(o2, explore=False, out=scratch, mean_out=mean)
+        if getattr(self, "_log_std_dev", None) is None:   # uploaded once (no host copy per call)
+            self._log_std_dev = t.as_tensor(self.w["log_std"], device=self.device)
+        log_std = self._log_std_dev
+        adi = out.get("action_dist_inputs")
+        if adi is None:
+            adi = t.empty(lead + (2 * self.n_out,), dtype=t.float32, device=self.device)
+        adi.view(R, 2 * self.n_out)[:, :self.n_out].copy_(mean)
+        adi.view(R, 2 * self.n_out)[:, self.n_out:].copy_(log_std.expand(R, self.n_out))
+        # DiagGaussian.logp (RLlib): -0.5 sum(((x - mean) / std)^2) - 0.5 log(2 pi) n_out - sum(log_std)
+        z = (actions.reshape(R, self.n_out) - mean) * t.exp(-log_std)
+        logp = -0.5 * (z * z).sum(-1) - 0.5 * np.log(2.0 * np.pi) * self.n_out - log_std.sum()
+        lp = out.get("action_logp")
+        if lp is None:
+            lp = t.empty(lead, dtype=t.float32, device=self.device)
+        lp.view(R).copy_(logp)
+        res = {"action_dist_inputs": adi, "action_logp": lp}
+        if value is not None:
+            if value.n_in != self.n_in or value.n_out != 1:
+                raise ValueError("sample_batch_columns: the value branch must map n_in -> 1")
+            vf = out.get("vf_preds")
+            if vf is None:
+                vf = t.empty(lead, dtype=t.float32, device=self.device)
+            value.act(o2, explore=False, out=t.empty(R, 1, dtype=t.float32, device=self.device), mean_out=vf.view(R, 1))
+            res["vf_preds"] = vf
+        return res
+
     def close(self):
         if getattr(self, "h", None):
             N.lib().hum_policy_destroy(self.h)

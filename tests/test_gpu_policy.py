@@ -324,6 +324,52 @@ def test_fused_rollout_rejects_other_kernels():
     pol.close()
 
 
+def test_sample_batch_columns_match_torch_fp32():
+    """The SampleBatch columns RLlib's sampler records (action_dist_inputs, action_logp, vf_preds) for a fused
+    rollout's recorded inputs and samples: the value branch and the policy mean against plain PyTorch fp32, the
+    log-density against torch.distributions.Normal summed over the action dimensions."""
+    n, k = 512, 8
+    pol = DevicePolicy.random_init(seed=9)
+    vpol = DevicePolicy.random_init_value(seed=12)
+    vpol.w["b3"][:] = 0.3
+    vpol.close()
+    vpol = DevicePolicy(vpol.w, n_out=1)
+    env = HumanoidVecEnv(n, clips=("motion02_04",), seed=2)
+    env.reset()
+    tr = pol.rollout(env, k, explore=True, step0=3, fused=True)
+    cols = pol.sample_batch_columns(tr["obs"], tr["actions"], value=vpol)
+    obs = tr["obs"].reshape(-1, 70)
+    mean = reference_mean(pol.w, obs)
+    vf = reference_mean(vpol.w, obs)[:, 0]
+    std = torch.exp(torch.as_tensor(pol.w["log_std"], device="cuda"))
+    logp = torch.distributions.Normal(mean, std).log_prob(tr["actions"].reshape(-1, 17)).sum(-1)
+    assert cols["action_dist_inputs"].shape == (k, n, 34) and cols["vf_preds"].shape == (k, n)
+    torch.testing.assert_close(cols["action_dist_inputs"].reshape(-1, 34)[:, :17], mean, atol=2e-5, rtol=0)
+    torch.testing.assert_close(cols["action_dist_inputs"].reshape(-1, 34)[:, 17:], torch.log(std).expand(len(obs), 17))
+    torch.testing.assert_close(cols["vf_preds"].reshape(-1), vf, atol=2e-5, rtol=0)
+    torch.testing.assert_close(cols["action_logp"].reshape(-1), logp, atol=2e-3, rtol=1e-5)
+    env.close()
+    pol.close()
+    vpol.close()
+
+
+def test_value_branch_from_rllib_weight_names():
+    rng = np.random.default_rng(0)
+    names = {"default_policy/fc_value_1/kernel": (70, 256), "default_policy/fc_value_1/bias": (256,),
+             "default_policy/fc_value_2/kernel": (256, 256), "default_policy/fc_value_2/bias": (256,),
+             "default_policy/value_out/kernel": (256, 1), "default_policy/value_out/bias": (1,),
+             "default_policy/fc_1/kernel": (70, 256)}
+    w = {k: rng.standard_normal(s).astype(np.float32) * 0.05 for k, s in names.items()}
+    v = DevicePolicy.value_from_rllib_weights(w)
+    assert v.n_out == 1 and np.array_equal(v.w["w3"], w["default_policy/value_out/kernel"])
+    obs = torch.randn(64, 70, device="cuda")
+    got = torch.empty(64, 1, device="cuda")
+    v.act(obs, mean_out=got)
+    ref = reference_mean(v.w, obs)
+    assert (got - ref).abs().max().item() < 2e-5
+    v.close()
+
+
 def test_rllib_weight_names():
     """from_rllib_weights picks the policy branch of an RLlib 1.2 TF FullyConnectedNetwork weight dict."""
     rng = np.random.default_rng(0)
