@@ -9,7 +9,8 @@
 // the same FCNet on the 44-dim high observation and the 2-dim heading action); any n_in <= 72, n_out <= 32 works.
 //
 // MI355X mapping: one block = 16 envs x 16 waves (1024 threads; 4096 envs = 256 blocks = one per CU, four waves
-// per SIMD).  Wave w owns the 16x16 output tile of columns 16w..16w+15 of each hidden layer (waves 0, 1 the two
+// per SIMD); batches of >= 64 K rows (a fragment's SampleBatch columns) take 64 rows per block, each wave reusing its
+// weight fragments over four 16-row tiles (157 KB of LDS: one block per CU, a quarter of the weight traffic per row).  Wave w owns the 16x16 output tile of columns 16w..16w+15 of each hidden layer (waves 0, 1 the two
 // tiles of the 17-wide output layer), computed on v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain).
 // Weights are re-laid out once at hum_policy_create into MFMA B-fragment order (per tile, per 4 k-steps, per lane
 // a float4), so a wave fetches a whole layer's operands with coalesced 16-byte loads issued before the first
@@ -97,18 +98,37 @@ __device__ inline f32x4 mfma_tile(const float* X, int ldx, const f32x4* b) {
     return acc;
 }
 
+// RT independent 16x16 tiles (row tiles rt at X + rt * 16 * ldx) against the same fragments, their k-step chains
+// interleaved so consecutive MFMAs do not wait on each other's results (each tile's k order is mfma_tile's)
+template <int NS, int RT>
+__device__ inline void mfma_tiles(const float* X, int ldx, const f32x4* b, f32x4 (&acc)[RT]) {
+    const int l = threadIdx.x & 63;
+    const float* xr = X + (l & 15) * ldx + (l >> 4);
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+            acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[rt * ROWS * ldx + 4 * s], b[s >> 2][s & 3], acc[rt], 0, 0, 0);
+}
+
+// RT row tiles of 16 per block: every wave reuses its B fragments over the RT tiles (RT = 4 for large batches:
+// a quarter of the L2 weight traffic per row; RT = 1 keeps one 16-row block per CU for a 4096-lane step)
+template <int RT>
 __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
-    __shared__ float xs[ROWS * PX];
-    __shared__ float h1[ROWS * PH];
-    __shared__ float h2[ROWS * PH];
+    constexpr int NR = ROWS * RT;
+    __shared__ float xs[NR * PX];
+    __shared__ float h1[NR * PH];
+    __shared__ float h2[NR * PH];
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
-    const int row0 = blockIdx.x * ROWS;
+    const int row0 = blockIdx.x * NR;
     // every fragment this wave needs, before anything waits (hidden layers: tile = wave; output layer: waves 0, 1)
     f32x4 b1f[SQ1], b2f[SQ2];
     load_frags<SQ1>(p.f1, wave, b1f);
     load_frags<SQ2>(p.f2, wave, b2f);
     // observation tile (done lanes read their post-reset observation: the sampler's next input)
-    for (int e = tid; e < ROWS * K1; e += blockDim.x) {
+    for (int e = tid; e < NR * K1; e += blockDim.x) {
         const int r = e / K1, k = e - r * K1, i = row0 + r;
         float v = 0.f;
         if (i < p.n && k < p.n_in) {
@@ -121,40 +141,51 @@ __global__ void __launch_bounds__(64 * WAVES) policy_kernel(PolicyArgs p) {
     __syncthreads();
     const int c = 16 * wave + (l & 15);   // C/D map: lane l, register q -> row 4 (l >> 4) + q, column l & 15
     {
-        const f32x4 acc = mfma_tile<K1 / 4>(xs, PX, b1f);
         const float bias = p.b1[c];
+        f32x4 acc[RT];
+        mfma_tiles<K1 / 4, RT>(xs, PX, b1f, acc);
 #pragma unroll
-        for (int q = 0; q < 4; q++) h1[(4 * (l >> 4) + q) * PH + c] = tanhf(acc[q] + bias);
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) h1[(rt * ROWS + 4 * (l >> 4) + q) * PH + c] = tanhf(acc[rt][q] + bias);
     }
     __syncthreads();
     {
-        const f32x4 acc = mfma_tile<H / 4>(h1, PH, b2f);
         const float bias = p.b2[c];
+        f32x4 acc[RT];
+        mfma_tiles<H / 4, RT>(h1, PH, b2f, acc);
 #pragma unroll
-        for (int q = 0; q < 4; q++) h2[(4 * (l >> 4) + q) * PH + c] = tanhf(acc[q] + bias);
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) h2[(rt * ROWS + 4 * (l >> 4) + q) * PH + c] = tanhf(acc[rt][q] + bias);
     }
     __syncthreads();
     if (wave < NT3 && 16 * wave < p.n_out) {   // output layer: up to two 16-wide tiles of columns, one per wave
         f32x4 b3f[SQ3];
         load_frags<SQ3>(p.f3, wave, b3f);
-        const f32x4 o = mfma_tile<H / 4>(h2, PH, b3f);
+        f32x4 oo[RT];
+        mfma_tiles<H / 4, RT>(h2, PH, b3f, oo);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = 4 * (l >> 4) + q, c3 = 16 * wave + (l & 15), i = row0 + r;
-            if (c3 < p.n_out && i < p.n) {
-                const float mean = o[q] + p.b3[c3];
-                float a = mean;
-                if (p.explore) {   // DiagGaussian sample: mean + exp(log_std) * N(0, 1), counter-based Box-Muller
-                    // (seed, lane, step, column) each through its own mixing round: no two triples share a draw
-                    const unsigned long long x = mix64(mix64(mix64(p.seed ^ (unsigned long long)i) ^ p.step) ^ (unsigned long long)c3);
-                    const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;   // (0, 1]
-                    const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
-                    a = mean + expf(p.log_std[c3]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+        for (int rt = 0; rt < RT; rt++) {
+            const f32x4 o = oo[rt];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = rt * ROWS + 4 * (l >> 4) + q, c3 = 16 * wave + (l & 15), i = row0 + r;
+                if (c3 < p.n_out && i < p.n) {
+                    const float mean = o[q] + p.b3[c3];
+                    float a = mean;
+                    if (p.explore) {   // DiagGaussian sample: mean + exp(log_std) * N(0, 1), counter-based Box-Muller
+                        // (seed, lane, step, column) each through its own mixing round: no two triples share a draw
+                        const unsigned long long x = mix64(mix64(mix64(p.seed ^ (unsigned long long)i) ^ p.step) ^ (unsigned long long)c3);
+                        const float u1 = ((float)(x >> 40) + 1.f) * 0x1.0p-24f;   // (0, 1]
+                        const float u2 = (float)((x >> 16) & 0xFFFFFFull) * 0x1.0p-24f;
+                        a = mean + expf(p.log_std[c3]) * sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+                    }
+                    const long o2 = (long)i * p.n_out + c3;
+                    p.act[o2] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
+                    if (p.raw_out) p.raw_out[o2] = a;           // the sample itself (SampleBatch actions)
+                    if (p.mean_out) p.mean_out[o2] = mean;
                 }
-                const long o = (long)i * p.n_out + c3;
-                p.act[o] = fminf(fmaxf(a, -1.f), 1.f);   // clip_actions (Box [-1, 1])
-                if (p.raw_out) p.raw_out[o] = a;           // the sample itself (SampleBatch actions)
-                if (p.mean_out) p.mean_out[o] = mean;
             }
         }
     }
@@ -256,7 +287,13 @@ int hum_policy_act_ex(hum_policy* p, const float* obs, const float* obs_reset, c
     a.obs = obs; a.obs_reset = obs_reset; a.done = done; a.act = actions; a.mean_out = mean_out; a.obs_in_out = obs_in_out;
     a.raw_out = raw_out;
     a.n = n; a.explore = explore; a.seed = p->seed; a.step = step; a.n_in = p->n_in; a.n_out = p->n_out;
-    hipLaunchKernelGGL(policy_kernel, dim3((n + ROWS - 1) / ROWS), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
+    // batches of 4 row tiles per block once there are at least 4 such blocks per CU (the batched SampleBatch columns
+    // over a fragment's k x n rows); a step's 4096 rows keep one 16-row block per CU
+    if (n >= 4 * ROWS * 4 * 256)
+        hipLaunchKernelGGL(policy_kernel<4>, dim3((n + 4 * ROWS - 1) / (4 * ROWS)), dim3(64 * WAVES), 0,
+                           (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(policy_kernel<1>, dim3((n + ROWS - 1) / ROWS), dim3(64 * WAVES), 0, (hipStream_t)stream, a);
     const hipError_t st = hipGetLastError();
     if (st != hipSuccess) return perr(HUM_ERR_HIP, std::string("hum_policy_act: ") + hipGetErrorString(st));
     return HUM_OK;

@@ -18,7 +18,7 @@ from ilrl_amd.policy import DevicePolicy, hier_rollout, reference_mean  # noqa: 
 from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
 
-@pytest.mark.parametrize("n", [1, 17, 4096])
+@pytest.mark.parametrize("n", [1, 17, 4096, 65536 + 77])   # the last: 4 row tiles per block (policy.hip), ragged end
 def test_policy_mean_matches_torch_fp32(n):
     pol = DevicePolicy.random_init(seed=3)
     pol.w["b1"][:] = np.linspace(-0.3, 0.3, 256)   # non-zero biases exercise every term
@@ -31,6 +31,10 @@ def test_policy_mean_matches_torch_fp32(n):
     ref = reference_mean(pol.w, obs)
     assert (mean - ref).abs().max().item() < 2e-5
     torch.testing.assert_close(act, ref.clamp(-1, 1), atol=2e-5, rtol=0)
+    if n > 4096:   # the 4-tile blocks equal the 1-tile kernel row for row (the same k-ordered MFMA chains)
+        m1 = torch.empty(4096, 17, device="cuda")
+        pol.act(obs[-4096:].contiguous(), mean_out=m1)
+        assert torch.equal(m1, mean[-4096:])
     pol.close()
 
 
