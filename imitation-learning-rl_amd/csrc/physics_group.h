@@ -501,10 +501,17 @@ static __shared__ unsigned long long s_tlast;   // shared: markers also sit insi
 #else
 #define SUBPHASE(k) do { } while (0)
 #endif
-// HUM_SUBPHASE_PGS: the Delassus PGS's own split (markers 19-22) in place of the post-step ones
+// HUM_SUBPHASE_PGS: the Delassus PGS's own split (markers 19-22) in place of the post-step ones; HUM_SUBPHASE_ROWS:
+// the rows phase's split (markers 19-22, per row round: setup, Jacobian, articulated solve, coupling)
+#define ROWS_SUBPHASE(k) do { } while (0)
 #ifdef HUM_SUBPHASE_PGS
 #define PGS_SUBPHASE(k) SUBPHASE(k)
 #define POST_SUBPHASE(k) do { } while (0)
+#elif defined(HUM_SUBPHASE_ROWS)
+#define PGS_SUBPHASE(k) do { } while (0)
+#define POST_SUBPHASE(k) do { } while (0)
+#undef ROWS_SUBPHASE
+#define ROWS_SUBPHASE(k) SUBPHASE(k)
 #else
 #define PGS_SUBPHASE(k) do { } while (0)
 #define POST_SUBPHASE(k) SUBPHASE(k)
@@ -914,11 +921,14 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             sc[2] = f == 0 ? (T)1e10 : T(0);   // friction rows: bounds come from mu * lambda_n in the PGS
             sc[5] = f == 0 ? T(0) : (bb >= 0 ? (T)P.mu_self : (T)P.mu_ground);   // friction rows only
         }
+        ROWS_SUBPHASE(19);
         g_row_jacobian2(S, ba, fa, bb, fb, J);   // limit rows: ba = bb = -1 -> J = 0 (unit entry below)
 #pragma unroll
         for (int k = 0; k < NDOF; k++)
             if (k == jd) J[6 + k] = jsign;
+        ROWS_SUBPHASE(20);
         g_response(S, J, Mi);
+        ROWS_SUBPHASE(21);
         T jm = 0;
 #pragma unroll
         for (int q = 0; q < NV; q++) jm += J[q] * Mi[q];   // limit rows: sg * Mi[6 + d] (sg^2 = 1)
@@ -934,7 +944,9 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
         if (lam) {
 #pragma unroll
             for (int q = 0; q < NV; q++) qc += J[q] * S.nu[q];
-        } else {
+        } else
+#ifndef HUM_COUPLING_LDS   // A/B: every coupling from the LDS pass below instead of the predecessor lane
+        {
             const int qr = p - epos, qp = qr == 0 ? pool_rows(enl, enc) - 1 : qr - 1;
             const int rp = qp < enl + enc ? qp : qp - pool_gap(enc);
             const int tp = (t - r) + rp, t0 = t - lane;
@@ -956,6 +968,10 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             }
             if (here) qc = c * sc[4];
         }
+#else
+        {}
+#endif
+        ROWS_SUBPHASE(22);
         if (p < cap) {
             int n3, n3ln;
             if (lam) {   // dense layout: the normal row of friction row r is row enl + (r - enl - enc) / 2
@@ -973,7 +989,12 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
     // couplings c_r = J_r . (M^-1 J^T)_pred(r) (cyclic predecessor; 0 after a zero row) for the lookahead
     // PGS, which needs them only when the block's rows all sit in LDS: the rows whose predecessor another round
     // solved (more rows than lanes), from LDS
-    if (!lam && pos[EPB_] <= cap && total > EPB_ * GL) {   // rows whose predecessor was solved in another round
+#ifdef HUM_COUPLING_LDS
+    constexpr bool all_lds = true;
+#else
+    constexpr bool all_lds = false;
+#endif
+    if (!lam && pos[EPB_] <= cap && (all_lds || total > EPB_ * GL)) {   // rows whose predecessor another round solved
         wave_sync();
         for (int t = lane; t < total; t += EPB_ * GL) {
             int e = 0;
@@ -986,7 +1007,7 @@ __device__ __attribute__((always_inline)) void group_rows(const PhysParams& P, G
             const int qr = pool_pos(r, enl, enc);
             const int qp = qr == 0 ? pool_rows(enl, enc) - 1 : qr - 1;
             const int tp = (t - r) + (qp < enl + enc ? qp : qp - pool_gap(enc));
-            if (!pool_zero(qp, enl, enc) && tp / (EPB_ * GL) != t / (EPB_ * GL)) {
+            if (!pool_zero(qp, enl, enc) && (all_lds || tp / (EPB_ * GL) != t / (EPB_ * GL))) {
                 T* Rr = reinterpret_cast<T*>(reinterpret_cast<char*>(shb) + pool_off<T>(epos + qr));
                 const T* Rp = reinterpret_cast<const T*>(reinterpret_cast<const char*>(shb) + pool_off<T>(epos + qp));
                 T c = 0;

@@ -87,19 +87,9 @@ __device__ inline void load_frags(const float* __restrict__ F, int t, f32x4* b) 
 #pragma unroll
     for (int q = 0; q < NSQ; q++) b[q] = src[q * 64];
 }
-// one 16x16 tile: acc = X[16 x 4*NS] (LDS, pitch ldx) times the tile's fragments, k-steps in order
-template <int NS>
-__device__ inline f32x4 mfma_tile(const float* X, int ldx, const f32x4* b) {
-    const int l = threadIdx.x & 63;
-    const float* xr = X + (l & 15) * ldx + (l >> 4);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < NS; s++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], b[s >> 2][s & 3], acc, 0, 0, 0);
-    return acc;
-}
-
-// RT independent 16x16 tiles (row tiles rt at X + rt * 16 * ldx) against the same fragments, their k-step chains
-// interleaved so consecutive MFMAs do not wait on each other's results (each tile's k order is mfma_tile's)
+// RT independent 16x16 tiles acc[rt] = X[rt 16 .. rt 16 + 15][0 .. 4 NS) (LDS, pitch ldx) times the tile's fragments;
+// each tile's k-steps in order (the k-ordered fp32 fma chain the fused kernels restate), the RT chains interleaved so
+// consecutive MFMAs do not wait on each other's results
 template <int NS, int RT>
 __device__ inline void mfma_tiles(const float* X, int ldx, const f32x4* b, f32x4 (&acc)[RT]) {
     const int l = threadIdx.x & 63;

@@ -94,6 +94,9 @@ subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1:
 if os.environ.get("PGS_SUB") == "1":   # HUM_SUBPHASE_PGS builds: the Delassus PGS's split instead of the post step's
     subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1: inertia+bias", 15: "pass3: base",
             19: "pgs: A operands", 20: "pgs: A MFMA", 21: "pgs: A stores + rows", 22: "pgs: sweeps"}
+if os.environ.get("ROWS_SUB") == "1":   # HUM_SUBPHASE_ROWS builds: the rows phase's split instead of the post step's
+    subn = {11: "fk: sin/cos", 12: "fk: chain", 13: "pass1: parent vel", 14: "pass1: inertia+bias", 15: "pass3: base",
+            19: "rows: setup + contact", 20: "rows: Jacobian", 21: "rows: M^-1 J^T solve", 22: "rows: jm + coupling"}
 if sub.any():
     print("sub-phase cycles per block-step (each taken out of its phase above): mean | slowest 1%")
     for k, nm in subn.items():
