@@ -1,5 +1,6 @@
-// group_f32.hip - the benchmarked kernel (cooperative, fp32, 4 envs per wavefront) compiled on its own
-// (see kernels.h for why it is a separate translation unit).
+// group_f32.hip - the cooperative fp32 kernel, 4 envs per wavefront, for either env (the hierarchical env's hot
+// kernel; the low-level env runs group_f32_low.hip's twin), compiled on its own (see kernels.h for why it is a
+// separate translation unit).
 #include "kernels.h"
 
 namespace hkk {

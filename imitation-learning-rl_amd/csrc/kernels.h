@@ -840,8 +840,9 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
 #ifndef HUM_GROUP_MIN_WAVES
 #define HUM_GROUP_MIN_WAVES 1
 #endif
-// POLICY: 0 = actions from a.act (hum_step_k / hum_hier_step_k), 1 = the low-level network inside the step loop
-// (hum_rollout_fused), 2 = both networks of the hierarchical env (hum_hier_rollout_fused)
+// POLICY: 0 = actions from a.act, either env (hum_step_k / hum_hier_step_k), 1 = the low-level network inside the step
+// loop (hum_rollout_fused), 2 = both networks of the hierarchical env (hum_hier_rollout_fused), 3 = actions from a.act,
+// the low-level env only (hum_step_k's benchmarked fp32 kernel: the hierarchical code compiled out)
 template <typename T, int EPB_, bool TERRAIN = false, int POLICY = 0>
 __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a0) {
     __shared__ GroupLDS<T> sh[EPB_];
@@ -897,7 +898,9 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     const int gbit = (tid & 63) & ~(GL - 1);
     const long io = (long)t * a.n + i;   // this step's input / output row of the env
     constexpr bool HP = POLICY == 2;
-    const bool hier = HP || a.hier;
+    constexpr bool NET = POLICY == 1 || POLICY == 2;       // a network acts inside the step loop
+    constexpr bool LOWONLY = POLICY == 3;   // the low-level env only (the launcher checks a.hier)
+    const bool hier = HP || (!LOWONLY && a.hier);
     if constexpr (HP) {
         // the two-level sampler's input (hum_hier_rollout's per-transition policy calls): an env expecting the high
         // agent reads its latest high observation (done at the previous transition: its auto-reset one), the others
@@ -971,13 +974,13 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     // POLICY: the env's clipped actions held in registers across the physics (which reuses the scratch), one per lane
     // (lane 0 also the 17th); post_step reads them back from LDS for the electricity cost
     float pact0 = 0.f, pact1 = 0.f;
-    if constexpr (POLICY != 0) {
+    if constexpr (NET) {
         pact0 = policy_scratch(S)[PACT_OFF + l];
         pact1 = policy_scratch(S)[PACT_OFF + GL];
     }
     bool fin = true;
     for (int k = l; k < HUM_NACT; k += GL) {   // apply_action (humanoid.py:54-60)
-        const float av = !valid ? 0.f : (POLICY ? policy_scratch(S)[PACT_OFF + k] : a.act[io * HUM_NACT + k]);
+        const float av = !valid ? 0.f : (NET ? policy_scratch(S)[PACT_OFF + k] : a.act[io * HUM_NACT + k]);
         fin = fin && isfinite(av);
         S.tau[M.act_dof[k]] = (T)motor_torque(a.np1, M.act_gain[k], M.act_gain_d[k], isfinite(av) ? av : 0.f);
     }
@@ -1018,7 +1021,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     float* rstage = reinterpret_cast<float*>(scs + 144);   // the auto-reset observation
     static_assert(sizeof(sh[0].x.aba.IA) >= (144 + HUM_NOBS) * sizeof(T) && 2 * NDOF + 2 + 2 * NDOF <= 72,
                   "output row staging");
-    if constexpr (POLICY != 0) {   // the step's actions for post_step, in the reset-obs staging row (written after it)
+    if constexpr (NET) {   // the step's actions for post_step, in the reset-obs staging row (written after it)
         rstage[l] = pact0;
         if (l == 0) rstage[GL] = pact1;
     }
@@ -1072,7 +1075,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             } else {
                 float act[HUM_NACT];
 #pragma unroll
-                for (int k = 0; k < HUM_NACT; k++) act[k] = POLICY ? rstage[k] : a.act[io * HUM_NACT + k];
+                for (int k = 0; k < HUM_NACT; k++) act[k] = NET ? rstage[k] : a.act[io * HUM_NACT + k];
                 post_step(a, i, io, st, b, act, ef, scs, &rst, ostage, jstage, jal_l);
             }
         }
@@ -1121,8 +1124,8 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         wave_sync();
         // the output rows, coalesced (POLICY: the next step's input stays in LDS; only the last step's rows go to
         // the handle's [n, 70] obs / obs_reset buffers)
-        const long orow_i = POLICY ? (long)i : io;
-        if (valid && (!POLICY || t == ksteps - 1)) {
+        const long orow_i = NET ? (long)i : io;
+        if (valid && (!NET || t == ksteps - 1)) {
             float* orow = a.obs + orow_i * HUM_NOBS;
             for (int k = l; k < HUM_NOBS; k += GL) orow[k] = ostage[k];
             if (sf >= 0 && a.obs_reset) {
@@ -1295,6 +1298,7 @@ __global__ void parts_kernel(KArgs a, double* out) {
 
 // the benchmarked cooperative kernel lives in its own translation unit (group_f32.hip)
 hipError_t launch_group_f32_4(const KArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_group_f32_4_low(const KArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_group_f32_4_policy(const KArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_group_f32_4_hier_policy(const KArgs& a, int nblocks, hipStream_t s);
 

@@ -54,7 +54,10 @@ def cmp(a, b):
         if not same:
             bad += 1
             d = np.abs(x.astype(np.float64) - y.astype(np.float64))
-            print("DIFF %-16s max |a-b| %.3g at %s" % (k, d.max(), np.unravel_index(d.argmax(), d.shape)))
+            idx = np.unravel_index(d.argmax(), d.shape)
+            nd = np.argwhere(d > 0)
+            print("DIFF %-16s max |a-b| %.3g at %s (a %r, b %r); %d entries differ, first at %s" % (
+                k, d.max(), idx, x[idx], y[idx], len(nd), tuple(nd[0]) if len(nd) else None))
     print("%d of %d arrays differ" % (bad, len(A.files)))
     return bad
 

@@ -17,7 +17,7 @@ SRC = os.path.join(REPO, "imitation-learning-rl_amd", "csrc", "humanoid_env.hip"
 # HOT=1: the shipped benchmarked kernel's translation unit and flags (csrc/Makefile HOTFLAGS)
 HOT = os.environ.get("HOT") == "1"
 if HOT:
-    SRC = os.path.join(REPO, "imitation-learning-rl_amd", "csrc", "group_f32.hip")
+    SRC = os.path.join(REPO, "imitation-learning-rl_amd", "csrc", "group_f32_low.hip")
 HOTFLAGS = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp", "-fno-slp-vectorize", "-mllvm", "-disable-machine-licm"]
 NAMES = {1: "fk", 2: "pass1", 3: "pass2", 4: "base+pass3", 5: "geom/limits", 6: "contacts", 7: "rows", 8: "pgs",
          9: "integrate", 10: "post_step"}
@@ -30,7 +30,7 @@ def main():
                           + (HOTFLAGS if HOT else [])
                           + os.environ.get("ISA_FLAGS", "").split())
     lines = open(out).read().split("\n")
-    st = [i for i, l in enumerate(lines) if re.match(r"_ZN3hkk17step_group_kernelIfLi4ELb0EL[bi]0EEEvNS_5KArgsE:", l)][0]
+    st = [i for i, l in enumerate(lines) if re.match(r"_ZN3hkk17step_group_kernelIfLi4ELb0ELi3EEEvNS_5KArgsE:", l)][0]
     en = [i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end")][0]
     cur = 0
     cnt = collections.defaultdict(collections.Counter)
