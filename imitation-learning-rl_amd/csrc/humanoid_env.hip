@@ -591,7 +591,7 @@ int launch_step(hum_env* e, const KArgs& a, hipStream_t s) {
 #endif
     if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != HUM_DIAG_EPB || e->terrain)
         return fail(HUM_ERR_ARG, "diagnostic build: only kernel 1, fp32, envs_per_block HUM_DIAG_EPB, plane");
-    if (a.hier) hipLaunchKernelGGL((step_group_kernel<float, HUM_DIAG_EPB>), dim3((e->n + HUM_DIAG_EPB - 1) / HUM_DIAG_EPB),
+    if (a.hier) hipLaunchKernelGGL((step_group_kernel<float, HUM_DIAG_EPB, false, 4>), dim3((e->n + HUM_DIAG_EPB - 1) / HUM_DIAG_EPB),
                                    dim3(HUM_DIAG_EPB * GL), 0, s, a);
     else hipLaunchKernelGGL((step_group_kernel<float, HUM_DIAG_EPB, false, 3>), dim3((e->n + HUM_DIAG_EPB - 1) / HUM_DIAG_EPB),
                             dim3(HUM_DIAG_EPB * GL), 0, s, a);
@@ -609,7 +609,7 @@ int launch_step(hum_env* e, const KArgs& a, hipStream_t s) {
         } else {
             if (epb == 4) {
 #ifdef HUM_SINGLE_TU
-                if (a.hier) hipLaunchKernelGGL((step_group_kernel<float, 4>), g, blk, 0, s, a);
+                if (a.hier) hipLaunchKernelGGL((step_group_kernel<float, 4, false, 4>), g, blk, 0, s, a);
                 else hipLaunchKernelGGL((step_group_kernel<float, 4, false, 3>), g, blk, 0, s, a);
 #else
                 if (a.hier) HIPCHK(launch_group_f32_4(a, (int)g.x, s));

@@ -840,9 +840,10 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
 #ifndef HUM_GROUP_MIN_WAVES
 #define HUM_GROUP_MIN_WAVES 1
 #endif
-// POLICY: 0 = actions from a.act, either env (hum_step_k / hum_hier_step_k), 1 = the low-level network inside the step
-// loop (hum_rollout_fused), 2 = both networks of the hierarchical env (hum_hier_rollout_fused), 3 = actions from a.act,
-// the low-level env only (hum_step_k's benchmarked fp32 kernel: the hierarchical code compiled out)
+// POLICY: 0 = actions from a.act, either env (hum_step_k / hum_hier_step_k: fp64, envs_per_block 1 / 2, terrain),
+// 1 = the low-level network inside the step loop (hum_rollout_fused), 2 = both networks of the hierarchical env
+// (hum_hier_rollout_fused), 3 = actions from a.act, the low-level env only (hum_step_k's benchmarked fp32 kernel),
+// 4 = actions from a.act, the hierarchical env only (hum_hier_step_k's fp32 kernel)
 template <typename T, int EPB_, bool TERRAIN = false, int POLICY = 0>
 __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_kernel(KArgs a0) {
     __shared__ GroupLDS<T> sh[EPB_];
@@ -899,8 +900,11 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
     const long io = (long)t * a.n + i;   // this step's input / output row of the env
     constexpr bool HP = POLICY == 2;
     constexpr bool NET = POLICY == 1 || POLICY == 2;       // a network acts inside the step loop
-    constexpr bool LOWONLY = POLICY == 3;   // the low-level env only (the launcher checks a.hier)
-    const bool hier = HP || (!LOWONLY && a.hier);
+    // the env-specialised instantiations compile the other env's branches out (bitwise equal, faster: DESIGN.md
+    // section 4); the generic one (POLICY 0) reads the env from the launch arguments
+    constexpr bool LOWONLY = POLICY == 1 || POLICY == 3;   // the low-level env only (the launchers check a.hier)
+    constexpr bool HIERONLY = POLICY == 2 || POLICY == 4;  // the hierarchical env only
+    const bool hier = HIERONLY || (!LOWONLY && a.hier);
     if constexpr (HP) {
         // the two-level sampler's input (hum_hier_rollout's per-transition policy calls): an env expecting the high
         // agent reads its latest high observation (done at the previous transition: its auto-reset one), the others
