@@ -11,7 +11,8 @@ for v in $VARS; do
   lib=$L/libhumenv_$v.so; [ $v = new ] && lib=$L/libhumenv.so
   ILRL_AMD_AB=1 ILRL_AMD_LIB=$lib timeout -k 10 200 python3 tools/diag_lib_bitwise.py dump $O/$v.npz >> $O/bit.log 2>&1 || { tail -5 $O/bit.log; exit 3; }
 done
-for v in $VARS; do echo "== head vs $v"; python3 tools/diag_lib_bitwise.py cmp $O/head.npz $O/$v.npz > $O/cmp_$v.txt; tail -1 $O/cmp_$v.txt; done
+BV=${VARS%% *}   # the first build is the bitwise reference
+for v in $VARS; do echo "== $BV vs $v"; python3 tools/diag_lib_bitwise.py cmp $O/$BV.npz $O/$v.npz > $O/cmp_$v.txt; tail -1 $O/cmp_$v.txt; done
 rm -f $O/*.npz
 for r in $(seq 1 ${REPS:-3}); do
   for v in $VARS; do
