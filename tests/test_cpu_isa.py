@@ -58,3 +58,20 @@ def test_no_flat_memory_instructions(tmp_path):
                 flat.append((fn, line.strip()[:80]))
     assert kernels >= 8
     assert not flat, "flat (generic-pointer) memory instructions: %s" % flat[:5]
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists(OBJDUMP), reason="needs the built library")
+def test_env_specialised_fp32_kernels_present(tmp_path):
+    """The fp32, 4-envs-per-block plane kernels are env-specialised: POLICY 1 (hum_rollout_fused),
+    2 (hum_hier_rollout_fused), 3 (hum_step_k, low-level env: the benchmarked kernel), 4 (hum_step_k, hierarchical
+    env); the generic POLICY 0 instantiation of that shape is no longer built (its launch paths moved to the twins)."""
+    names = set()
+    for j, co in enumerate(code_objects(LIB)):
+        f = tmp_path / ("co_%d.o" % j)
+        f.write_bytes(co)
+        dis = subprocess.check_output([OBJDUMP, "-d", str(f)], text=True)
+        names |= {line.split("<")[-1][:-2] for line in dis.splitlines() if line.endswith(">:")}
+    pre = "_ZN3hkk17step_group_kernelIfLi4ELb0EL"
+    for pol in (1, 2, 3, 4):
+        assert "%si%dEEEvNS_5KArgsE" % (pre, pol) in names, "POLICY %d fp32 kernel missing" % pol
+    assert "%si0EEEvNS_5KArgsE" % pre not in names
