@@ -235,10 +235,11 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             high = DevicePolicy.random_init_high(seed=17 + rank, device=dev.index)
             low = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
             traj_out = {}   # by launch size: the trajectory rows, reused launch to launch (allocated before the clock)
+            mtr = bool(a.sample_batch and a.fused)   # the fused kernel records the policy means (no recompute)
             acted = {}      # by launch number: the agent that acted per (transition, lane), counted after the clock
 
             def traj_bufs(kk, s):
-                o = dict(traj_out.setdefault(kk, hier_traj_buffers(n, kk, dev)))
+                o = dict(traj_out.setdefault(kk, hier_traj_buffers(n, kk, dev, means=mtr)))
                 o["acted"] = acted.setdefault(s + soff[0], torch.empty(kk, n, dtype=torch.uint8, device=dev))
                 return o
 
@@ -250,11 +251,13 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
 
             def step(s, kk=k):   # launch numbers (and the exploration noise's step index) continue past the warm-up
                 tr = hier_rollout(env, high, low, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True,
-                                  fused=a.fused, out=traj_bufs(kk, s))
+                                  fused=a.fused, out=traj_bufs(kk, s), means=mtr)
                 if a.sample_batch:   # both agents' columns over all rows (the acting agent's rows are the valid ones)
                     ch, cl = cols_out.setdefault(kk, ({}, {}))
-                    ch.update(high.sample_batch_columns(tr["obs_high"], tr["act_high"], value=vhigh, out=ch))
-                    cl.update(low.sample_batch_columns(tr["obs_low"], tr["act_low"], value=vlow, out=cl))
+                    ch.update(high.sample_batch_columns(tr["obs_high"], tr["act_high"], value=vhigh, out=ch,
+                                                        mean=tr.get("mean_high")))
+                    cl.update(low.sample_batch_columns(tr["obs_low"], tr["act_low"], value=vlow, out=cl,
+                                                       mean=tr.get("mean_low")))
                 return tr
             env._bench_acted = acted
     else:
@@ -286,11 +289,12 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
                 def step(s, kk=k):
                     o = traj_out.get(kk)
                     tr = pol.rollout(env, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True, fused=True,
-                                     out=o)
+                                     out=o, means=a.sample_batch)
                     traj_out.setdefault(kk, tr)
-                    if a.sample_batch:
+                    if a.sample_batch:   # the means recorded by the fused kernel: no policy recompute
                         c = cols_out.setdefault(kk, {})
-                        c.update(pol.sample_batch_columns(tr["obs"], tr["actions"], value=vpol, out=c))
+                        c.update(pol.sample_batch_columns(tr["obs"], tr["actions"], value=vpol, out=c,
+                                                          mean=tr["means"]))
                     return tr
     env.reset()
     env.done.zero_()
@@ -318,6 +322,8 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
                 traj_out[kk] = {"obs": torch.empty(kk, n, 70, device=dev), "actions": torch.empty(kk, n, 17, device=dev),
                                 "rewards": torch.empty(kk, n, device=dev),
                                 "dones": torch.empty(kk, n, dtype=torch.uint8, device=dev)}
+                if a.sample_batch:
+                    traj_out[kk]["means"] = torch.empty(kk, n, 17, device=dev)
     if not a.policy:
         # every output buffer the timed launches write exists before the clock starts (a warmup shorter than k, e.g.
         # the driver's --steps 20 --warmup 5, never ran a launch of the timed shape: its allocation and zero fill

@@ -847,7 +847,7 @@ __attribute__((visibility("hidden"))) int hum_internal_device(const hum_env* e) 
 __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
     hum_env* e, const float* pw, uint64_t seed, int32_t k, int32_t explore, uint64_t step0, float* obs, float* obs_reset,
     uint8_t* done, float* reward, float* act_last, float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj,
-    void* stream) {
+    float* mean_traj, void* stream) {
     if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != 4 || e->terrain != HUM_TERRAIN_PLANE ||
         e->cfg.hier)
         return fail(HUM_ERR_STATE, "hum_rollout_fused: needs the cooperative fp32 kernel, 4 envs per block, plane ground "
@@ -888,6 +888,7 @@ __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
     a.obs_traj = obs_traj;
     a.act_traj = act_traj;
     a.act_last = act_last;
+    a.mean_traj = mean_traj;
     const int nb = (e->n + 3) / 4;
 #ifndef HUM_DIAG_F32_ONLY
     hipError_t st = launch_group_f32_4_policy(a, nb, s);
@@ -907,7 +908,8 @@ __attribute__((visibility("hidden"))) int hum_internal_rollout_fused(
 // stream-ordered: every call on one handle must use one stream, or order its streams with events)
 __attribute__((visibility("hidden"))) int hum_internal_hier_rollout_fused(
     hum_env* e, const float* pw_high, uint64_t seed_high, const float* pw_low, uint64_t seed_low, int32_t k,
-    int32_t explore, uint64_t step0, const hum_hier_io* io, const hum_hier_traj* T, void* stream) {
+    int32_t explore, uint64_t step0, const hum_hier_io* io, const hum_hier_traj* T, float* mean_high, float* mean_low,
+    void* stream) {
     if (e->cfg.kernel != 1 || e->cfg.precision || e->cfg.envs_per_block != 4 || e->terrain != HUM_TERRAIN_PLANE ||
         !e->cfg.hier)
         return fail(HUM_ERR_STATE, "hum_hier_rollout_fused: needs a hierarchical handle on the cooperative fp32 kernel, "
@@ -958,6 +960,8 @@ __attribute__((visibility("hidden"))) int hum_internal_hier_rollout_fused(
     a.obs_traj_high = T->obs_high;
     a.act_traj_high = T->act_high;
     a.act_last_high = io->act_high;
+    a.mean_traj = mean_low;
+    a.mean_traj_high = mean_high;
     a.pstep0 = step0;
     a.pexplore = explore;
     const int nb = (e->n + 3) / 4;

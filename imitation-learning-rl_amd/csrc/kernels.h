@@ -90,6 +90,10 @@ struct KArgs {
     float* obs_traj_high;
     float* act_traj_high;
     float* act_last_high;
+    // optional [ksteps, n, 17] / [ksteps, n, 2]: the policy means (RLlib's action_dist_inputs mean half) of the acting
+    // envs, as the networks form them before the DiagGaussian sample (hum_rollout_fused_ex / hum_hier_rollout_fused_ex)
+    float* mean_traj;
+    float* mean_traj_high;
 };
 
 // CustomHumanoidRobot.apply_action torque of motor k (humanoid.py:54-60): float(force_gain * power * 0.41 *
@@ -766,7 +770,7 @@ __device__ __attribute__((always_inline)) inline void policy_hidden(HUM_LDS floa
 template <typename T, int EPB_, int NIN = HUM_NOBS, int NOUT = HUM_NACT>
 __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, GroupLDS<T>* sh, int blk, int t, const float* pw,
                                                            unsigned long long pseed, unsigned long long emask,
-                                                           float* act_traj, float* act_last) {
+                                                           float* act_traj, float* act_last, float* mean_traj) {
     static_assert(EPB_ * 16 == 64, "policy_wave: one (env, column) chain per lane");
     static_assert(NOUT == 17 || NOUT * EPB_ <= 64, "policy_wave: output chains");
     const int lane = threadIdx.x & 63;
@@ -826,6 +830,7 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
         if (i < a.n) {
             const long io = (long)t * a.n + i;
             if (act_traj) act_traj[io * NOUT + c] = v;   // the sample before clip_actions (SampleBatch)
+            if (mean_traj) mean_traj[io * NOUT + c] = mean;   // the distribution's mean (action_dist_inputs)
             if (act_last && t == a.ksteps - 1) act_last[(long)i * NOUT + c] = pa[c];
         }
     };
@@ -939,8 +944,8 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         // each network only for the envs that act with it; a network no env of the wave needs is skipped
         const unsigned long long hm = __ballot(l == 0 && hi), lm = __ballot(l == 0 && valid && !hi);
         if (hm) policy_wave<T, EPB_, HUM_NOBS_HIGH, HUM_NACT_HIGH>(a, sh, blk, t, a.pw_high, a.pseed_high, hm,
-                                                                    a.act_traj_high, a.act_last_high);
-        if (lm) policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, lm, a.act_traj, a.act_last);
+                                                                    a.act_traj_high, a.act_last_high, a.mean_traj_high);
+        if (lm) policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, lm, a.act_traj, a.act_last, a.mean_traj);
     } else if constexpr (POLICY == 1) {
         // the sampler's input: step 0 the handle's current observation (a lane done at the previous step: its reset
         // observation), later steps the row the previous step staged (its reset row if it reset)
@@ -973,7 +978,7 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
             }
         }
         wave_sync();
-        policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, ~0ull, a.act_traj, a.act_last);
+        policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, ~0ull, a.act_traj, a.act_last, a.mean_traj);
     }
     // POLICY: the env's clipped actions held in registers across the physics (which reuses the scratch), one per lane
     // (lane 0 also the 17th); post_step reads them back from LDS for the electricity cost

@@ -28,13 +28,14 @@ void hum_internal_set_error(const char* msg);
 int hum_internal_device(const hum_env* env);   // humanoid_env.hip
 int hum_internal_rollout_fused(hum_env* e, const float* pw, uint64_t seed, int32_t k, int32_t explore, uint64_t step0,
                                float* obs, float* obs_reset, uint8_t* done, float* reward, float* act_last,
-                               float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj, void* stream);
+                               float* obs_traj, float* act_traj, float* rew_traj, uint8_t* done_traj,
+                               float* mean_traj, void* stream);
 int hum_internal_hier_step_acted(hum_env* e, const float* high_act, const float* low_act, uint8_t* agents,
                                  float* high_obs, float* low_obs, float* high_rew, float* low_rew, uint8_t* done,
                                  uint32_t flags, float* high_obs_reset, uint8_t* acted, void* stream);
 int hum_internal_hier_rollout_fused(hum_env* e, const float* pw_high, uint64_t seed_high, const float* pw_low,
                                     uint64_t seed_low, int32_t k, int32_t explore, uint64_t step0, const hum_hier_io* io,
-                                    const hum_hier_traj* T, void* stream);
+                                    const hum_hier_traj* T, float* mean_high, float* mean_low, void* stream);
 
 namespace {
 
@@ -324,9 +325,9 @@ int hum_rollout(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_
     return HUM_OK;
 }
 
-int hum_rollout_fused(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_t step0, float* obs,
-                      float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
-                      float* rew_traj, uint8_t* done_traj, void* stream) {
+int hum_rollout_fused_ex(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_t step0, float* obs,
+                         float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj,
+                         float* act_traj, float* rew_traj, uint8_t* done_traj, float* mean_traj, void* stream) {
     if (!env || !p || k <= 0 || !obs || !obs_reset || !done || !reward || !act_buf)
         return perr(HUM_ERR_ARG, "hum_rollout_fused: bad argument");
     if (p->n_in != HUM_NOBS || p->n_out != HUM_NACT)
@@ -334,7 +335,14 @@ int hum_rollout_fused(hum_env* env, hum_policy* p, int32_t k, int32_t explore, u
     if (hum_internal_device(env) != p->device)
         return perr(HUM_ERR_ARG, "hum_rollout_fused: the env handle and the policy are on different devices");
     return hum_internal_rollout_fused(env, p->w, p->seed, k, explore, step0, obs, obs_reset, done, reward, act_buf,
-                                      obs_traj, act_traj, rew_traj, done_traj, stream);
+                                      obs_traj, act_traj, rew_traj, done_traj, mean_traj, stream);
+}
+
+int hum_rollout_fused(hum_env* env, hum_policy* p, int32_t k, int32_t explore, uint64_t step0, float* obs,
+                      float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
+                      float* rew_traj, uint8_t* done_traj, void* stream) {
+    return hum_rollout_fused_ex(env, p, k, explore, step0, obs, obs_reset, done, reward, act_buf, obs_traj, act_traj,
+                                rew_traj, done_traj, nullptr, stream);
 }
 
 }  // extern "C"
@@ -398,12 +406,18 @@ int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k,
 
 // hum_hier_rollout in one launch: both networks inside the cooperative kernel's step loop, each evaluated only for
 // the envs that act with it (a wave whose four envs all expect the low agent skips the high network and vice versa)
-int hum_hier_rollout_fused(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
-                           const hum_hier_io* io, const hum_hier_traj* tr, void* stream) {
+int hum_hier_rollout_fused_ex(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore,
+                              uint64_t step0, const hum_hier_io* io, const hum_hier_traj* tr, float* mean_high,
+                              float* mean_low, void* stream) {
     if (const int rc = hier_rollout_check("hum_hier_rollout_fused", env, high, low, k, io)) return rc;
     const hum_hier_traj none = {};
     return hum_internal_hier_rollout_fused(env, high->w, high->seed, low->w, low->seed, k, explore, step0, io,
-                                           tr ? tr : &none, stream);
+                                           tr ? tr : &none, mean_high, mean_low, stream);
+}
+
+int hum_hier_rollout_fused(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore, uint64_t step0,
+                           const hum_hier_io* io, const hum_hier_traj* tr, void* stream) {
+    return hum_hier_rollout_fused_ex(env, high, low, k, explore, step0, io, tr, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

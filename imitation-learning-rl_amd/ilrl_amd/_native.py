@@ -13,10 +13,10 @@ LIB_PATH = os.environ.get("ILRL_AMD_LIB", DEFAULT_LIB_PATH)
 # signatures are unchanged - later ones only added entry points).  Without it every library, override or not,
 # must match HUM_ABI_VERSION and export every symbol.
 AB_MODE = os.environ.get("ILRL_AMD_AB") == "1"
-AB_COMPATIBLE_ABIS = (8, 9, 10, 11)   # ABI 10 added hum_policy_create_ex, hum_hier_rollout; 11 hum_pack_rows;
-# 12 hum_hier_rollout_fused
+AB_COMPATIBLE_ABIS = (8, 9, 10, 11, 12)   # ABI 10 added hum_policy_create_ex, hum_hier_rollout; 11 hum_pack_rows;
+# 12 hum_hier_rollout_fused; 13 hum_rollout_fused_ex, hum_hier_rollout_fused_ex (the policy mean traces)
 
-HUM_ABI_VERSION = 12   # include/humanoid_env.h
+HUM_ABI_VERSION = 13   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
@@ -52,7 +52,8 @@ EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_creat
            "hum_reset_ex", "hum_hier_reset_ex", "hum_clip_csv_sizes", "hum_clip_csv_parse", "hum_load_clip_csv",
            "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout", "hum_rollout_fused", "hum_set_terrain",
            "hum_step_k", "hum_hier_step_k", "hum_set_terrain_ex", "hum_policy_act_ex", "hum_policy_create_ex",
-           "hum_hier_rollout", "hum_pack_rows", "hum_hier_rollout_fused"]
+           "hum_hier_rollout", "hum_pack_rows", "hum_hier_rollout_fused", "hum_rollout_fused_ex",
+           "hum_hier_rollout_fused_ex"]
 
 
 class HumConfig(ctypes.Structure):
@@ -138,12 +139,14 @@ def lib():
     L.hum_policy_create_ex.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(vp)]
     L.hum_hier_rollout.argtypes = [vp, vp, vp, i32, i32, u64, ctypes.POINTER(HumHierIO), ctypes.POINTER(HumHierTraj), vp]
     L.hum_hier_rollout_fused.argtypes = L.hum_hier_rollout.argtypes
+    L.hum_hier_rollout_fused_ex.argtypes = L.hum_hier_rollout.argtypes[:-1] + [vp, vp, vp]
     L.hum_policy_destroy.argtypes = [vp]
     L.hum_pack_rows.argtypes = [ctypes.POINTER(HumPackField), i32, i32, i32, i32, vp]
     L.hum_policy_act.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, u64, vp]
     L.hum_policy_act_ex.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, i32, u64, vp]
     L.hum_rollout.argtypes = [vp, vp, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.hum_rollout_fused.argtypes = [vp, vp, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.hum_rollout_fused_ex.argtypes = [vp, vp, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.hum_hier_reset_ex.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.hum_step.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, vp]
     L.hum_step_k.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp, i32, vp]

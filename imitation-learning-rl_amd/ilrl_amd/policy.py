@@ -112,21 +112,26 @@ class DevicePolicy:
              "w3": _normc(rng, (H, 1), 0.01), "b3": np.zeros(1)}
         return cls(w, device=device, seed=seed, n_in=n_in, n_out=1)
 
-    def sample_batch_columns(self, obs, actions, value=None, out=None):
+    def sample_batch_columns(self, obs, actions, value=None, out=None, mean=None):
         """The policy-side SampleBatch columns RLlib's sampler records per step, for recorded policy inputs obs
         [..., n_in] and raw samples actions [..., n_out] (device; e.g. a rollout's trajectory, any leading shape):
         action_dist_inputs [..., 2 n_out] (the DiagGaussian's mean and log_std), action_logp [...] (log-density of
         the raw sample) and, given the value branch `value` (a 1-output DevicePolicy), vf_preds [...].  One
         policy launch (and one value launch) over all rows: within a fragment the weights are fixed, so this equals
-        what the per-step compute_actions records.  out: a dict of the same tensors to write into."""
+        what the per-step compute_actions records.  out: a dict of the same tensors to write into.  mean: the policy
+        means of these rows when the rollout already recorded them (rollout / hier_rollout with means=True: bitwise
+        what the policy launch would give), so no policy launch runs."""
         t = self.torch
         lead = tuple(obs.shape[:-1])
         R = int(np.prod(lead)) if lead else 1
         o2 = obs.reshape(R, self.n_in)
         out = out if out is not None else {}
-        mean = t.empty(R, self.n_out, dtype=t.float32, device=self.device)
-        scratch = t.empty(R, self.n_out, dtype=t.float32, device=self.device)   # the clipped actions (unused)
-        self.act(o2, explore=False, out=scratch, mean_out=mean)
+        if mean is None:
+            mean = t.empty(R, self.n_out, dtype=t.float32, device=self.device)
+            scratch = t.empty(R, self.n_out, dtype=t.float32, device=self.device)   # the clipped actions (unused)
+            self.act(o2, explore=False, out=scratch, mean_out=mean)
+        else:
+            mean = mean.reshape(R, self.n_out)
         if getattr(self, "_log_std_dev", None) is None:   # uploaded once (no host copy per call)
             self._log_std_dev = t.as_tensor(self.w["log_std"], device=self.device)
         log_std = self._log_std_dev
@@ -181,21 +186,27 @@ class DevicePolicy:
                 "hum_policy_act")
         return act
 
-    def rollout(self, venv, k, explore=True, step0=0, trajectories=True, fused=False, out=None):
+    def rollout(self, venv, k, explore=True, step0=0, trajectories=True, fused=False, out=None, means=False):
         """k sampler steps (policy -> env step with auto-reset) on venv's lanes, all on the device with no host
         round trip.  venv.obs must hold the current observation (after venv.reset()).  Returns the trajectory
         tensors {obs [k,n,70] (policy inputs), actions [k,n,17] (the samples before clip_actions, as RLlib records
         them), rewards [k,n], dones [k,n]} (or {}).  fused: one launch with the policy inside the step kernel
         (hum_rollout_fused; cooperative fp32 handles with 4 envs per block on the plane).  out: a dict of the same
-        tensors to write into (reused across calls, e.g. by a timed loop) instead of fresh ones."""
+        tensors to write into (reused across calls, e.g. by a timed loop) instead of fresh ones.  means (fused only):
+        also means [k,n,17], the policy's mean per step as the in-kernel network forms it (hum_rollout_fused_ex), for
+        sample_batch_columns(..., mean=...)."""
         t = self.torch
         n = venv.n
+        if means and not (fused and trajectories):
+            raise ValueError("rollout: means=True needs fused=True and trajectories=True")
         if not hasattr(venv, "_act_buf"):
             venv._act_buf = t.zeros(n, N.HUM_NACT, dtype=t.float32, device=venv.device)
         tr = {}
         if trajectories:
             shapes = {"obs": ((N.HUM_NOBS,), t.float32), "actions": ((N.HUM_NACT,), t.float32),
                       "rewards": ((), t.float32), "dones": ((), t.uint8)}
+            if means:
+                shapes["means"] = ((N.HUM_NACT,), t.float32)
             for f, (sh, dt) in shapes.items():
                 x = out.get(f) if out else None
                 if x is None:
@@ -205,11 +216,14 @@ class DevicePolicy:
                                      % (f, dt, (k, n) + sh, venv.device))
                 tr[f] = x
         p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
-        fn = N.lib().hum_rollout_fused if fused else N.lib().hum_rollout
-        N.check(fn(venv.h, self.h, k, int(bool(explore)), ctypes.c_uint64(step0), p(venv.obs),
-                   p(venv.obs_reset), p(venv.done), p(venv.reward), p(venv._act_buf),
-                   p(tr.get("obs")), p(tr.get("actions")), p(tr.get("rewards")), p(tr.get("dones")),
-                   venv._stream()), "hum_rollout_fused" if fused else "hum_rollout")
+        args = (venv.h, self.h, k, int(bool(explore)), ctypes.c_uint64(step0), p(venv.obs), p(venv.obs_reset),
+                p(venv.done), p(venv.reward), p(venv._act_buf), p(tr.get("obs")), p(tr.get("actions")),
+                p(tr.get("rewards")), p(tr.get("dones")))
+        if means:
+            N.check(N.lib().hum_rollout_fused_ex(*args, p(tr["means"]), venv._stream()), "hum_rollout_fused_ex")
+        else:
+            fn = N.lib().hum_rollout_fused if fused else N.lib().hum_rollout
+            N.check(fn(*args, venv._stream()), "hum_rollout_fused" if fused else "hum_rollout")
         return tr
 
 
@@ -221,13 +235,17 @@ def _hier_traj_shapes():
             "rew_high": ((), f32), "rew_low": ((), f32), "done": ((), u8)}
 
 
-def hier_traj_buffers(n, k, device):
-    """Fresh trajectory tensors for hier_rollout(..., out=...) of k transitions on n lanes."""
+def hier_traj_buffers(n, k, device, means=False):
+    """Fresh trajectory tensors for hier_rollout(..., out=..., means=means) of k transitions on n lanes."""
     import torch as t
-    return {f: t.empty((k, n) + sh, dtype=dt, device=device) for f, (sh, dt) in _hier_traj_shapes().items()}
+    out = {f: t.empty((k, n) + sh, dtype=dt, device=device) for f, (sh, dt) in _hier_traj_shapes().items()}
+    if means:
+        out["mean_high"] = t.empty(k, n, N.HUM_NACT_HIGH, dtype=t.float32, device=device)
+        out["mean_low"] = t.empty(k, n, N.HUM_NACT, dtype=t.float32, device=device)
+    return out
 
 
-def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True, fused=False, out=None):
+def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True, fused=False, out=None, means=False):
     """k transitions of the two-level env venv (a HierVecEnv after reset()) with the high-level policy `high`
     (44 -> 2) and the low-level policy `low` (70 -> 17), all on the device (hum_hier_rollout): per transition each
     lane steps with the action of the agent it expects.  venv's buffers carry the state between calls (obs_high /
@@ -236,15 +254,23 @@ def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True, f
     rew_high [k,n], rew_low [k,n], done [k,n]} (or {}).
     fused: one launch with both networks inside the env kernel (hum_hier_rollout_fused; the obs / act rows of the
     agent that did not act on a lane are left unwritten).  out: a dict of the same tensors to write into (reused
-    across calls, e.g. by a timed loop) instead of fresh ones."""
+    across calls, e.g. by a timed loop) instead of fresh ones.  means (fused only): also mean_high [k,n,2] and
+    mean_low [k,n,17], the acting agent's policy mean per transition (hum_hier_rollout_fused_ex; the other agent's
+    rows unwritten), for sample_batch_columns(..., mean=...)."""
     import torch as t
     n, dev = venv.n, venv.device
+    if means and not (fused and trajectories):
+        raise ValueError("hier_rollout: means=True needs fused=True and trajectories=True")
     if not hasattr(venv, "_act_high_buf"):
         venv._act_high_buf = t.zeros(n, N.HUM_NACT_HIGH, dtype=t.float32, device=dev)
         venv._act_low_buf = t.zeros(n, N.HUM_NACT, dtype=t.float32, device=dev)
     tr = {}
     if trajectories:
-        for f, (sh, dt) in _hier_traj_shapes().items():
+        shapes = dict(_hier_traj_shapes())
+        if means:
+            shapes["mean_high"] = ((N.HUM_NACT_HIGH,), t.float32)
+            shapes["mean_low"] = ((N.HUM_NACT,), t.float32)
+        for f, (sh, dt) in shapes.items():
             x = out.get(f) if out else None
             if x is None:
                 x = t.empty((k, n) + sh, dtype=dt, device=dev)
@@ -256,10 +282,14 @@ def hier_rollout(venv, high, low, k, explore=True, step0=0, trajectories=True, f
     io = N.HumHierIO(p(venv.obs_high), p(venv.obs_high_reset), p(venv.obs), p(venv.done), p(venv.agents),
                      p(venv.reward_high), p(venv.reward), p(venv._act_high_buf), p(venv._act_low_buf))
     traj = N.HumHierTraj(*[p(tr.get(f)) for f, _ in N.HumHierTraj._fields_]) if trajectories else None
-    fn = "hum_hier_rollout_fused" if fused else "hum_hier_rollout"
-    N.check(getattr(N.lib(), fn)(venv.h, high.h, low.h, k, int(bool(explore)), ctypes.c_uint64(step0),
-                                 ctypes.byref(io), ctypes.byref(traj) if traj is not None else None,
-                                 venv._stream()), fn)
+    args = (venv.h, high.h, low.h, k, int(bool(explore)), ctypes.c_uint64(step0), ctypes.byref(io),
+            ctypes.byref(traj) if traj is not None else None)
+    if means:
+        N.check(N.lib().hum_hier_rollout_fused_ex(*args, p(tr["mean_high"]), p(tr["mean_low"]), venv._stream()),
+                "hum_hier_rollout_fused_ex")
+    else:
+        fn = "hum_hier_rollout_fused" if fused else "hum_hier_rollout"
+        N.check(getattr(N.lib(), fn)(*args, venv._stream()), fn)
     return tr
 
 

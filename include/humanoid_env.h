@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 12
+#define HUM_ABI_VERSION 13
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -364,6 +364,13 @@ int hum_rollout(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, ui
 int hum_rollout_fused(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
                       float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj, float* act_traj,
                       float* rew_traj, uint8_t* done_traj, void* stream);
+/* hum_rollout_fused with one more optional trace (ABI 13): mean_traj [k,n,17], the policy's mean per step and lane
+ * (the DiagGaussian's loc, the first half of RLlib's action_dist_inputs) as the in-kernel network forms it before the
+ * sample - bitwise what hum_policy_act_ex's mean_out gives for the same observation row.  With it a SampleBatch's
+ * action_dist_inputs / action_logp need no second network evaluation. */
+int hum_rollout_fused_ex(hum_env* env, hum_policy* policy, int32_t k, int32_t explore, uint64_t step0, float* obs,
+                         float* obs_reset, uint8_t* done, float* reward, float* act_buf, float* obs_traj,
+                         float* act_traj, float* rew_traj, uint8_t* done_traj, float* mean_traj, void* stream);
 
 /* ---- Two-level sampler loop (BASELINE config 5; hier_env.py:355-366, 538-642 driven by the reference's two PPO
  * policies, train_config.py:262-298 policy_mapping_fn: "high_level_agent" -> high_level_policy (44 -> 2),
@@ -413,6 +420,12 @@ int hum_hier_rollout(hum_env* env, hum_policy* high, hum_policy* low, int32_t k,
  * handle must use one stream (or order its streams with events). */
 int hum_hier_rollout_fused(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore,
                            uint64_t step0, const hum_hier_io* io, const hum_hier_traj* traj, void* stream);
+/* hum_hier_rollout_fused with the two policies' mean traces (ABI 13, each optional): mean_high [k,n,2], mean_low
+ * [k,n,17], written for the acting agent's rows only (the other agent's rows are left unwritten), bitwise what
+ * hum_policy_act_ex's mean_out gives for the recorded observation row. */
+int hum_hier_rollout_fused_ex(hum_env* env, hum_policy* high, hum_policy* low, int32_t k, int32_t explore,
+                              uint64_t step0, const hum_hier_io* io, const hum_hier_traj* traj, float* mean_high,
+                              float* mean_low, void* stream);
 
 /* RewardLogCallback terms (custom_callback.py:43-80) per lane: device float32 [n, HUM_NAUX]. */
 int hum_get_aux(hum_env* env, float* aux_out, void* stream);

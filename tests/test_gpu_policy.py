@@ -272,6 +272,64 @@ def test_hier_rollout_fused_equals_hier_rollout(n, k):
     low.close()
 
 
+def test_fused_rollout_mean_trace():
+    """hum_rollout_fused_ex's mean trace: every recorded mean equals the standalone policy kernel's mean on the
+    recorded input bitwise, the other outputs equal a run without the trace (same start state), and
+    sample_batch_columns with the recorded means equals the recomputing call bitwise."""
+    n, k = 512, 16
+    pol = DevicePolicy.random_init(seed=9)
+    envs = [HumanoidVecEnv(n, clips=("motion02_04",), seed=2) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    tm = pol.rollout(envs[0], k, explore=True, step0=7, fused=True, means=True)
+    tp = pol.rollout(envs[1], k, explore=True, step0=7, fused=True)
+    for f in ("obs", "actions", "rewards", "dones"):
+        assert torch.equal(tm[f], tp[f]), f
+    mean = torch.empty(n, 17, device="cuda")
+    for t in range(k):
+        pol.act(tm["obs"][t], explore=False, out=torch.empty(n, 17, device="cuda"), mean_out=mean)
+        torch.testing.assert_close(tm["means"][t], mean, atol=0, rtol=0)
+    c0 = pol.sample_batch_columns(tm["obs"], tm["actions"])
+    c1 = pol.sample_batch_columns(tm["obs"], tm["actions"], mean=tm["means"])
+    for f in ("action_dist_inputs", "action_logp"):
+        torch.testing.assert_close(c1[f], c0[f], atol=0, rtol=0, msg=f)
+    with pytest.raises(ValueError):
+        pol.rollout(envs[1], k, fused=False, means=True)
+    for x in envs:
+        x.close()
+    pol.close()
+
+
+def test_hier_rollout_fused_mean_traces():
+    """hum_hier_rollout_fused_ex: on each transition the acting agent's recorded mean equals its policy kernel's
+    mean on the recorded input bitwise, and the trajectory equals a fused run without the traces."""
+    n, k = 512, 20
+    high = DevicePolicy.random_init_high(seed=11)
+    low = DevicePolicy.random_init(seed=9)
+    envs = [HierVecEnv(n, seed=4) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    tm = hier_rollout(envs[0], high, low, k, explore=True, step0=3, fused=True, means=True)
+    tp = hier_rollout(envs[1], high, low, k, explore=True, step0=3, fused=True)
+    hi = tm["acted"] == N.HUM_AGENT_HIGH
+    lo = tm["acted"] == N.HUM_AGENT_LOW
+    assert hi.any() and lo.any()
+    for f in ("acted", "agents", "rew_high", "rew_low", "done"):
+        assert torch.equal(tm[f], tp[f]), f
+    for f, m in (("obs_high", hi), ("act_high", hi), ("obs_low", lo), ("act_low", lo)):
+        torch.testing.assert_close(tm[f][m], tp[f][m], atol=0, rtol=0, msg=f)
+    for pol, obs, mt, m, no in ((high, tm["obs_high"], tm["mean_high"], hi, 2), (low, tm["obs_low"], tm["mean_low"], lo, 17)):
+        rows = obs[m]
+        mean = torch.empty(rows.shape[0], no, device="cuda")
+        pol.act(rows.contiguous(), explore=False, out=torch.empty_like(mean), mean_out=mean)
+        torch.testing.assert_close(mt[m], mean, atol=0, rtol=0)
+    for x in envs:
+        assert x.error_flags() == 0
+        x.close()
+    high.close()
+    low.close()
+
+
 def test_hier_rollout_fused_without_trajectory():
     """No trajectory rows: the per-transition agents / rewards / done go to the handle's scratch (grown on demand),
     and the env buffers and the state still equal the per-transition loop's, call after call."""
