@@ -767,7 +767,10 @@ __device__ __attribute__((always_inline)) inline void policy_hidden(HUM_LDS floa
 // NIN -> 256 -> 256 -> NOUT: the low-level network (70 -> 17, weights pw, seed pseed) or the hierarchical env's
 // high-level one (44 -> 2); emask: bit GL e set = env e of the wave acts with this network (the others' results are
 // dropped: a wave whose envs expect different agents runs both networks, each keeping its own envs' actions)
-template <typename T, int EPB_, int NIN = HUM_NOBS, int NOUT = HUM_NACT>
+// COMPACT (the two-level kernel, whose emask varies per wave): the hidden layers run for the acting envs only - each
+// env's chains are separate instructions (policy_hidden's per-env accumulators), so a network needed by one env of
+// the wave costs a quarter of the full one; every chain keeps its k order (bitwise the same values)
+template <typename T, int EPB_, int NIN = HUM_NOBS, int NOUT = HUM_NACT, bool COMPACT = false>
 __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, GroupLDS<T>* sh, int blk, int t, const float* pw,
                                                            unsigned long long pseed, unsigned long long emask,
                                                            float* act_traj, float* act_last, float* mean_traj) {
@@ -785,10 +788,30 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
 #pragma unroll
     for (int e = 0; e < EPB_; e++) F[e] = (HUM_LDS float*)policy_scratch(sh[e]);
     // hidden layer 1 (K = NIN: policy.hip's zero rows NIN .. 71 add exact zeros), hidden layer 2
-    policy_hidden<EPB_, NIN, (NIN % 10 == 0 ? 10 : 11)>(F, W1, B1, PX_OFF, PH1_OFF, lane);
-    wave_sync();
-    policy_hidden<EPB_, 256, 16>(F, W2, B2, PH1_OFF, PH2_OFF, lane);
-    wave_sync();
+    auto hidden = [&](auto ne_c, HUM_LDS float* const (&Fa)[decltype(ne_c)::value]) {
+        constexpr int NE = decltype(ne_c)::value;
+        policy_hidden<NE, NIN, (NIN % 10 == 0 ? 10 : 11)>(Fa, W1, B1, PX_OFF, PH1_OFF, lane);
+        wave_sync();
+        policy_hidden<NE, 256, 16>(Fa, W2, B2, PH1_OFF, PH2_OFF, lane);
+        wave_sync();
+    };
+    if constexpr (COMPACT && EPB_ == 4) {
+        // the acting envs in ascending order (emask is wave-uniform: scalar bit arithmetic)
+        unsigned m = 0;
+#pragma unroll
+        for (int e = 0; e < EPB_; e++) m |= (unsigned)((emask >> (GL * e)) & 1ull) << e;
+        const int i0 = __builtin_ctz(m | 16u), m1 = m & (m - 1), i1 = __builtin_ctz(m1 | 16u);
+        const int m2 = m1 & (m1 - 1), i2 = __builtin_ctz(m2 | 16u);
+        auto Fi = [&](int e) { return (HUM_LDS float*)policy_scratch(sh[e < EPB_ ? e : 0]); };
+        switch (__builtin_popcount(m)) {
+            case 1: { HUM_LDS float* const Fa[1] = {Fi(i0)}; hidden(std::integral_constant<int, 1>{}, Fa); break; }
+            case 2: { HUM_LDS float* const Fa[2] = {Fi(i0), Fi(i1)}; hidden(std::integral_constant<int, 2>{}, Fa); break; }
+            case 3: { HUM_LDS float* const Fa[3] = {Fi(i0), Fi(i1), Fi(i2)}; hidden(std::integral_constant<int, 3>{}, Fa); break; }
+            default: hidden(std::integral_constant<int, EPB_>{}, F); break;
+        }
+    } else {
+        hidden(std::integral_constant<int, EPB_>{}, F);
+    }
     // output layer: 17 wide: chain A = (env lane / 16, column lane % 16), chain B = (env lane, column 16) in lanes
     // < EPB_; narrower: chain A = (env lane / NOUT, column lane % NOUT) in lanes < EPB_ NOUT
     constexpr bool WIDE = NOUT == 17;
@@ -943,9 +966,10 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
         wave_sync();
         // each network only for the envs that act with it; a network no env of the wave needs is skipped
         const unsigned long long hm = __ballot(l == 0 && hi), lm = __ballot(l == 0 && valid && !hi);
-        if (hm) policy_wave<T, EPB_, HUM_NOBS_HIGH, HUM_NACT_HIGH>(a, sh, blk, t, a.pw_high, a.pseed_high, hm,
+        if (hm) policy_wave<T, EPB_, HUM_NOBS_HIGH, HUM_NACT_HIGH, true>(a, sh, blk, t, a.pw_high, a.pseed_high, hm,
                                                                     a.act_traj_high, a.act_last_high, a.mean_traj_high);
-        if (lm) policy_wave<T, EPB_>(a, sh, blk, t, a.pw, a.pseed, lm, a.act_traj, a.act_last, a.mean_traj);
+        if (lm) policy_wave<T, EPB_, HUM_NOBS, HUM_NACT, true>(a, sh, blk, t, a.pw, a.pseed, lm, a.act_traj, a.act_last,
+                                                             a.mean_traj);
     } else if constexpr (POLICY == 1) {
         // the sampler's input: step 0 the handle's current observation (a lane done at the previous step: its reset
         // observation), later steps the row the previous step staged (its reset row if it reset)
