@@ -767,6 +767,9 @@ __device__ __attribute__((always_inline)) inline void policy_hidden(HUM_LDS floa
 // NIN -> 256 -> 256 -> NOUT: the low-level network (70 -> 17, weights pw, seed pseed) or the hierarchical env's
 // high-level one (44 -> 2); emask: bit GL e set = env e of the wave acts with this network (the others' results are
 // dropped: a wave whose envs expect different agents runs both networks, each keeping its own envs' actions)
+#ifndef HUM_PH2_UNROLL
+#define HUM_PH2_UNROLL 16   // the 256 x 256 layer's unroll (weight loads in flight)
+#endif
 // COMPACT (the two-level kernel, whose emask varies per wave): the hidden layers run for the acting envs only - each
 // env's chains are separate instructions (policy_hidden's per-env accumulators), so a network needed by one env of
 // the wave costs a quarter of the full one; every chain keeps its k order (bitwise the same values)
@@ -792,7 +795,7 @@ __device__ __attribute__((always_inline)) void policy_wave(const KArgs& a, Group
         constexpr int NE = decltype(ne_c)::value;
         policy_hidden<NE, NIN, (NIN % 10 == 0 ? 10 : 11)>(Fa, W1, B1, PX_OFF, PH1_OFF, lane);
         wave_sync();
-        policy_hidden<NE, 256, 16>(Fa, W2, B2, PH1_OFF, PH2_OFF, lane);
+        policy_hidden<NE, 256, HUM_PH2_UNROLL>(Fa, W2, B2, PH1_OFF, PH2_OFF, lane);
         wave_sync();
     };
     if constexpr (COMPACT && EPB_ == 4) {
