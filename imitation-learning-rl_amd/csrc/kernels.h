@@ -494,8 +494,9 @@ __device__ __attribute__((always_inline)) void hier_post(const KArgs& a, int i, 
     bool done = false;
     float rew_low = 0.f, rew_high = 0.f;
     if (high) {
-        // cur_obs is the last calc_state (same physics state, walk target before this call)
-        calc_state(st, b.wt, obs, js, jal, pp);
+        // cur_obs is the last calc_state (same physics state, walk target before this call); scs: the cooperative
+        // kernel's hinge sin / cos of this (unchanged) state, the same hinge_sincos values forward_kinematics forms
+        calc_state(st, b.wt, obs, js, jal, pp, scs);
         const float a0 = hact ? hact[0] : a.act_high[2 * io], a1 = hact ? hact[1] : a.act_high[2 * io + 1];
         const float actionDegree = (float)atan2((double)a1, (double)a0) * (float)RAD2DEG;   // :540 (float32)
         const double newDegree = (double)actionDegree + pp.yaw * RAD2DEG;                   // :543
@@ -1101,11 +1102,11 @@ __global__ void __launch_bounds__(EPB_ * GL, HUM_GROUP_MIN_WAVES) step_group_ker
                 float lact[HUM_NACT];
 #pragma unroll
                 for (int k = 0; k < HUM_NACT; k++) lact[k] = rstage[k];
-                hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs, false, (long)i, lact, lact);
+                hier_post(a, i, io, st, b, high, ef, scs, false, (long)i, lact, lact);
 #pragma unroll
                 for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];   // an auto-reset replaced it
             } else if (a.hier) {
-                hier_post(a, i, io, st, b, high, ef, high ? nullptr : scs, false);
+                hier_post(a, i, io, st, b, high, ef, scs, false);
 #pragma unroll
                 for (int e = 0; e < HUM_NSTATE; e++) S.st[e] = st[e];   // an auto-reset replaced it
             } else {
