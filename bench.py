@@ -232,6 +232,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:   # config 5 closed loop: both levels' policies on the device (hum_hier_rollout[_fused])
             from ilrl_amd.policy import DevicePolicy, hier_rollout, hier_traj_buffers
+            from ilrl_amd import _native as N
             high = DevicePolicy.random_init_high(seed=17 + rank, device=dev.index)
             low = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
             traj_out = {}   # by launch size: the trajectory rows, reused launch to launch (allocated before the clock)
@@ -252,12 +253,15 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             def step(s, kk=k):   # launch numbers (and the exploration noise's step index) continue past the warm-up
                 tr = hier_rollout(env, high, low, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True,
                                   fused=a.fused, out=traj_bufs(kk, s), means=mtr)
-                if a.sample_batch:   # both agents' columns over all rows (the acting agent's rows are the valid ones)
+                if a.sample_batch:   # both agents' columns; rows of the agent that did not act are zeroed
                     ch, cl = cols_out.setdefault(kk, ({}, {}))
+                    acted_k = tr["acted"]
                     ch.update(high.sample_batch_columns(tr["obs_high"], tr["act_high"], value=vhigh, out=ch,
-                                                        mean=tr.get("mean_high")))
+                                                        mean=tr.get("mean_high"),
+                                                        valid=(acted_k & N.HUM_AGENT_HIGH) != 0))
                     cl.update(low.sample_batch_columns(tr["obs_low"], tr["act_low"], value=vlow, out=cl,
-                                                       mean=tr.get("mean_low")))
+                                                       mean=tr.get("mean_low"),
+                                                       valid=(acted_k & N.HUM_AGENT_LOW) != 0))
                 return tr
             env._bench_acted = acted
     else:

@@ -125,7 +125,16 @@ class TrajectoryGather:
 
     def pack(self, slot, t0, outputs):
         """outputs: {field: [k, n, ...] time-major tensor of steps t0 .. t0 + k - 1 of the fragment}.  On the device
-        one hum_pack_rows launch copies every field (the HIP library's packing kernel); on the host, torch copies."""
+        one hum_pack_rows launch copies every field (the HIP library's packing kernel); on the host, torch copies.
+        Every field must hold the same k steps and 0 <= t0, t0 + k <= G: the packing kernel writes rows by offset and
+        knows nothing of the fragment's capacity, so a crossing pack is refused here on both paths."""
+        t0 = int(t0)
+        ks = {int(x.shape[0]) for x in outputs.values()}
+        if len(ks) != 1:
+            raise ValueError("pack: every field needs the same leading step count, got %s" % sorted(ks))
+        k = ks.pop()
+        if t0 < 0 or t0 + k > self.G:
+            raise ValueError("pack: steps [%d, %d) cross the fragment of %d steps" % (t0, t0 + k, self.G))
         if self.work[slot] is not None:   # the slot's previous gather must have read the buffer
             self.work[slot].wait()
             self.work[slot] = None

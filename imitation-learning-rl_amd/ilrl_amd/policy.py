@@ -112,7 +112,7 @@ class DevicePolicy:
              "w3": _normc(rng, (H, 1), 0.01), "b3": np.zeros(1)}
         return cls(w, device=device, seed=seed, n_in=n_in, n_out=1)
 
-    def sample_batch_columns(self, obs, actions, value=None, out=None, mean=None):
+    def sample_batch_columns(self, obs, actions, value=None, out=None, mean=None, valid=None):
         """The policy-side SampleBatch columns RLlib's sampler records per step, for recorded policy inputs obs
         [..., n_in] and raw samples actions [..., n_out] (device; e.g. a rollout's trajectory, any leading shape):
         action_dist_inputs [..., 2 n_out] (the DiagGaussian's mean and log_std), action_logp [...] (log-density of
@@ -120,7 +120,11 @@ class DevicePolicy:
         policy launch (and one value launch) over all rows: within a fragment the weights are fixed, so this equals
         what the per-step compute_actions records.  out: a dict of the same tensors to write into.  mean: the policy
         means of these rows when the rollout already recorded them (rollout / hier_rollout with means=True: bitwise
-        what the policy launch would give), so no policy launch runs."""
+        what the policy launch would give), so no policy launch runs.
+        valid: a bool mask of the leading shape marking the rows that hold a real transition.  A fused hierarchical
+        rollout (hier_rollout(fused=True)) leaves the non-acting agent's obs / act / mean rows unwritten, so their
+        columns would be computed from stale or uninitialised memory: pass valid = (acted & HUM_AGENT_x) != 0 there;
+        the invalid rows' columns are written as zeros."""
         t = self.torch
         lead = tuple(obs.shape[:-1])
         R = int(np.prod(lead)) if lead else 1
@@ -146,6 +150,11 @@ class DevicePolicy:
         lp = out.get("action_logp")
         if lp is None:
             lp = t.empty(lead, dtype=t.float32, device=self.device)
+        vm = None
+        if valid is not None:
+            vm = valid.reshape(R).to(t.bool)
+            logp = t.where(vm, logp, t.zeros((), dtype=logp.dtype, device=logp.device))
+            adi.view(R, 2 * self.n_out).masked_fill_(~vm[:, None], 0.0)
         lp.view(R).copy_(logp)
         res = {"action_dist_inputs": adi, "action_logp": lp}
         if value is not None:
@@ -155,6 +164,8 @@ class DevicePolicy:
             if vf is None:
                 vf = t.empty(lead, dtype=t.float32, device=self.device)
             value.act(o2, explore=False, out=t.empty(R, 1, dtype=t.float32, device=self.device), mean_out=vf.view(R, 1))
+            if vm is not None:
+                vf.view(R).masked_fill_(~vm, 0.0)
             res["vf_preds"] = vf
         return res
 

@@ -56,7 +56,7 @@ from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
 FP32_FLOOR = {"obs": 1e-5, "reward": 1e-5}
 FP32_RATIO = 1.5
 FP32_REALISATIONS = 4
-FP32_LANES = 512   # per config; config 2 (the benchmarked workload, k = 1 and k = 32) twice as many
+FP32_LANES = 512   # config 5's physics transitions; configs 2 (k = 1 and k = 32) and 3 twice as many
 # The floor of these ratios: another fp32 realisation of the oracle itself against the 4-realisation envelope measures
 # p50 0.72, p90 1.2, p99 1.9 - 2.3, max 3 - 4.4 on joint speeds (512 and 2048 lanes, the bench's states); the p99 over
 # 512 lanes (the 5th largest ratio) varies by +-0.5 between state samples for one build, hence 1024 lanes for config 2.
@@ -233,7 +233,7 @@ def test_full_size_rollout_no_drop_and_sample_matches_oracle(config, precision, 
     """k = 32: the benchmark's launch shape (4096 lanes, 32 env steps per hum_step_k launch)."""
     clips = ("motion02_04",) if config == "c2" else tuple(CLIP_NAMES)
     # fp32: the per-block maxima are compared over FP32_LANES lanes (per clip: 64 for the four-clip config 3)
-    per_clip = FP32_LANES * (2 if config == "c2" else 1) // len(clips) if precision == "fp32" else 64
+    per_clip = 2 * FP32_LANES // len(clips) if precision == "fp32" else 64
     flags, st = rollout_and_compare(clips, precision, steps=192 if k > 1 else 200, k=k, per_clip=per_clip)
     assert flags & N.HUM_EFLAG_CONTACT_OVERFLOW == 0, "a contact was dropped"
     assert flags & N.HUM_EFLAG_NONFINITE_ACTION == 0
@@ -308,8 +308,11 @@ def _agents_of(robs):
 
 
 def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23):
-    """per_kind lanes of each transition kind; the fp32 test takes FP32_LANES // 2 of each (the high-level ones take
-    no physics step: their low-level obs errors are 0)"""
+    """per_kind lanes of each transition kind (an int, or {1: high-level, 0: low-level}); the fp32 test takes
+    FP32_LANES low-level (physics) transitions for the per-lane gate and HIER_HIGH_LANES high-level ones, which take no
+    physics step and are held to their own absolute bound (HIER_HIGH_BOUND)"""
+    if isinstance(per_kind, int):
+        per_kind = {1: per_kind, 0: per_kind}
     from ilrl_amd.hier_env import HierVecEnv, HIER_CLIP
     clip = load_clip(HIER_CLIP)
     env = HierVecEnv(n, seed=seed, precision=precision)
@@ -342,8 +345,8 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
     prng32 = np.random.default_rng(17)
     for kind in (1, 0):   # high-level transition, low-level (physics) transition
         lanes = np.nonzero(expect == kind)[0]
-        assert len(lanes) >= per_kind
-        for i in lanes[np.linspace(0, len(lanes) - 1, per_kind).astype(int)]:
+        assert len(lanes) >= per_kind[kind]
+        for i in lanes[np.linspace(0, len(lanes) - 1, per_kind[kind]).astype(int)]:
             act = {OH.HIGH: ah[i]} if kind else {OH.LOW: al[i]}
             o = OH.OracleHierEnv.from_lane(clip, phys[i], book[i], BK)
             robs, rrew, rdone, _ = o.step(act)
@@ -402,13 +405,39 @@ def hier_rollout_and_compare(precision, n=4096, steps=200, per_kind=64, seed=23)
     return flags, {k: (np.array(v) if isinstance(v, list) else v) for k, v in st.items()}
 
 
+def _subset(st, m):
+    """the per-lane entries of a rollout_and_compare / hier_rollout_and_compare record restricted to mask m"""
+    out = {k: (v[m] if isinstance(v, np.ndarray) and v.shape[:1] == m.shape else v) for k, v in st.items()}
+    out["lanes"] = int(m.sum())
+    return out
+
+
+# config 5's high-level transitions take no physics step: their outputs (high obs 44, both rewards) come from the
+# unchanged state through calc_state / the drift score, so an fp32 kernel is held to SURVEY's tolerances directly
+HIER_HIGH_LANES = 128
+HIER_HIGH_BOUND = {"obs_max": 1e-5, "reward_max": 1e-5}
+
+
 @pytest.mark.parametrize("precision", ["fp32", "fp64"])
 def test_hier_full_size_rollout_sample_matches_oracle(precision):
-    """Config 5 at full size: 4096 lanes, 200 auto-reset transitions, then 64 high-level and 64 low-level
-    transitions vs the oracle from the injected lane state (hier_env.py:355-366, 538-642)."""
-    flags, st = hier_rollout_and_compare(precision, per_kind=FP32_LANES // 2 if precision == "fp32" else 64)
+    """Config 5 at full size: 4096 lanes, 200 auto-reset transitions, then high-level and low-level transitions vs
+    the oracle from the injected lane state (hier_env.py:355-366, 538-642).  fp32: the per-lane gate runs over the
+    FP32_LANES low-level (physics) transitions only - the high-level ones have no physics error and would dilute its
+    quantiles - and the high-level ones are bounded absolutely (HIER_HIGH_BOUND)."""
+    per_kind = {1: HIER_HIGH_LANES, 0: FP32_LANES} if precision == "fp32" else 64
+    flags, st = hier_rollout_and_compare(precision, per_kind=per_kind)
     assert flags & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
     assert st["exact_ok"], "agents / frame / timestep / RNG counter / level counters differ from the oracle"
+    if precision == "fp32":
+        high = st["kind"] == 1
+        sh = _summary("c5_fp32_high", _subset(st, high))
+        assert sh["obs_max"] <= HIER_HIGH_BOUND["obs_max"], sh["obs_max"]
+        assert sh["reward_max"] <= HIER_HIGH_BOUND["reward_max"], sh["reward_max"]
+        assert sh["done_mismatch"] == 0
+        s = _summary("c5_fp32", _subset(st, ~high))   # physics transitions only
+        assert s["lanes"] >= FP32_LANES
+        _check_fp32(s)
+        return
     s = _summary("c5_%s" % precision, st)
     if precision == "fp64":
         assert s["state_max"] < FP64_BOUND["state_max"]

@@ -55,3 +55,21 @@ def test_pack_rows_rejects_bad_descriptors():
     arr = (N.HumPackField * 1)(f)
     assert N.lib().hum_pack_rows(arr, 1, 4, 8, 0, ctypes.c_void_p(0)) == N.HUM_ERR_ARG
     assert N.lib().hum_pack_rows(arr, 0, 4, 8, 0, ctypes.c_void_p(0)) == N.HUM_ERR_ARG
+
+
+@pytest.mark.parametrize("dev_type", ["cuda", "cpu"])
+def test_pack_refuses_a_launch_crossing_the_fragment(dev_type):
+    """hum_pack_rows writes by offset and knows nothing of the fragment's capacity: TrajectoryGather.pack refuses
+    t0 < 0, t0 + k > G and fields of different step counts before anything is written, on both paths."""
+    dev = torch.device(dev_type, 0) if dev_type == "cuda" else torch.device("cpu")
+    n, G = 16, 8
+    tg = TrajectoryGather([("obs", (70,), torch.float32), ("done", (), torch.uint8)], [n], G, dev)
+    before = tg.send[0].clone()
+    mk = lambda k: {"obs": torch.ones(k, n, 70, device=dev), "done": torch.ones(k, n, dtype=torch.uint8, device=dev)}
+    for t0, k in ((4, 5), (8, 1), (-1, 2)):
+        with pytest.raises(ValueError):
+            tg.pack(0, t0, mk(k))
+    with pytest.raises(ValueError):
+        tg.pack(0, 0, {"obs": torch.ones(2, n, 70, device=dev), "done": torch.ones(3, n, dtype=torch.uint8, device=dev)})
+    assert torch.equal(tg.send[0], before)
+    tg.pack(0, 4, mk(4))   # exactly filling the fragment is fine

@@ -141,3 +141,21 @@ def test_gloo_world2_trajectory_gather_fragments(n_total):
         np.testing.assert_array_equal(f["act"][:, :nsteps], (v[..., None] - np.arange(17)).astype(np.float32))
         np.testing.assert_array_equal(f["done"][:, :nsteps], ((lane + t) % 2 == 0).astype(np.uint8))
         np.testing.assert_array_equal(f["frame"][:, :nsteps], (v * (1 << 33)).astype(np.int64))
+
+
+def test_trajectory_gather_pack_bounds_host():
+    """TrajectoryGather.pack refuses a launch that crosses the fragment (host path; the device path is
+    tests/test_gpu_traj_pack.py): 0 <= t0, t0 + k <= G, one step count for every field."""
+    import torch
+    from ilrl_amd.parallel import TrajectoryGather
+    n, G = 4, 8
+    tg = TrajectoryGather([("obs", (3,), torch.float32), ("done", (), torch.uint8)], [n], G, "cpu")
+    mk = lambda k: {"obs": torch.ones(k, n, 3), "done": torch.ones(k, n, dtype=torch.uint8)}
+    for t0, k in ((4, 5), (8, 1), (-1, 2)):
+        with pytest.raises(ValueError):
+            tg.pack(0, t0, mk(k))
+    with pytest.raises(ValueError):
+        tg.pack(0, 0, {"obs": torch.ones(2, n, 3), "done": torch.ones(3, n, dtype=torch.uint8)})
+    assert int(tg.send[0].abs().sum()) == 0
+    tg.pack(0, 4, mk(4))
+    assert int(tg.send[0].sum()) > 0
