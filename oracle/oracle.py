@@ -164,6 +164,19 @@ def phys_step(state, tau_motor, params=None, precision="fp64"):
     return st
 
 
+def ridge_contacts(a, b, r, params):
+    """A capsule (axis a-b, radius r) against the heightfield's convex edges (physics_oracle.c ridge_contacts):
+    [(normal (3), signed distance, axis parameter t)] per ridge contact."""
+    out = np.zeros(10)
+    dp = ctypes.POINTER(ctypes.c_double)
+    f = lib().om_ridge_contacts
+    f.argtypes = [ctypes.POINTER(OmParams), dp, dp, ctypes.c_double, dp]
+    f.restype = ctypes.c_int
+    n = f(ctypes.byref(params), _p(np.ascontiguousarray(a, dtype=np.float64)),
+          _p(np.ascontiguousarray(b, dtype=np.float64)), float(r), _p(out))
+    return [(out[5 * k:5 * k + 3].copy(), float(out[5 * k + 3]), float(out[5 * k + 4])) for k in range(n)]
+
+
 def parts(state):
     out = np.zeros((33, 3))
     st = np.ascontiguousarray(state, dtype=np.float64)
@@ -185,9 +198,12 @@ def mass_matrix(state):
     return H
 
 
+MAX_CONTACTS = 119   # physics_oracle.c MAXC: 29 ground points + 24 terrain ridge points + 66 geom pairs
+
+
 def contacts(state, params=None):
     P = params or default_params()
-    out = np.zeros((95, 12))
+    out = np.zeros((MAX_CONTACTS, 12))
     n = lib().om_contacts(ctypes.byref(P), _p(np.ascontiguousarray(state, dtype=np.float64)), _p(out))
     return out[:n]
 

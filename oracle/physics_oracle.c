@@ -93,9 +93,10 @@ static void to_rparams(const om_params* P, rparams* Q) {
 }
 
 #define NV (6 + OM_ND)
-/* contact list capacity: every candidate fits (29 sphere / capsule-end ground points + 66 geom pairs = 95), so
-   the default max_contacts never truncates (Bullet has no global contact cap) */
-#define MAXC 95
+/* contact list capacity: every candidate fits (29 sphere / capsule-end ground points + 2 terrain ridge points per
+   capsule (12 capsules) + 66 geom pairs = 119), so the default max_contacts never truncates (Bullet has no global
+   contact cap) */
+#define MAXC 119
 #define MAXROW (3 * MAXC + 2 * OM_ND)
 
 
@@ -613,6 +614,132 @@ static int terrain_contact(const rparams* P, const real* c, real r, real* n, rea
     return *d < P->contact_thresh;
 }
 
+/* closest points between segments p1q1 and p2q2 with their parameters s (on p1q1) and t (on p2q2); the same
+   clamping as seg_seg */
+static void seg_seg_st(const real* p1, const real* q1, const real* p2, const real* q2, real* c1, real* c2, real* s_out,
+                       real* t_out);
+
+/* Capsule bodies against the heightfield: ridge contacts ("What's missing" 1).
+ * Bullet collides a capsule with btHeightfieldTerrainShape through btConvexConcaveCollisionAlgorithm: every triangle
+ * under the capsule's AABB gets a convex-triangle closest-point query, and the points go into one persistent manifold
+ * (at most 4 points, breaking threshold 0.02).  Restated statelessly: the contacts of a capsule are the local minima of
+ * the distance from its axis to the surface.  Along the axis over a planar facet that distance is linear, across a
+ * concave edge it is the minimum of two linear functions (no interior minimum), so the minima are the two axis ends -
+ * the end-cap candidates the plane also uses (terrain_contact) - and the points where the axis passes over a CONVEX
+ * edge (a ridge: a block's top edge).  For every interior grid edge within reach of the capsule whose two triangles
+ * meet convexly (the second triangle's far vertex more than RIDGE_FLAT = 1e-5 m below the first's plane):
+ *   (s, e) = closest points of the axis [a, b] and the edge; kept when s is interior to the axis, more than the
+ *   breaking threshold from both ends (nearer, the end cap is that contact), when the edge point is the surface's
+ *   closest point to s (terrain_contact at s finds no face closer than |s - e| - 1e-5 m, or s lies inside the terrain)
+ *   and when terrain_contact's signed distance at s is below contact_thresh; the contact is terrain_contact's at s.
+ * Candidates within the breaking threshold of a kept one (the same convex vertex reached from two edges) are dropped;
+ * at most RIDGE_MAX per capsule (with the two end caps, Bullet's 4-point manifold), a deeper candidate replacing the
+ * shallowest kept.  Edge order: vertex rows j, then vertices i, then the horizontal, vertical and diagonal edge of
+ * vertex (i, j).  The same walk in csrc/terrain.h (ridge_contacts).  PyBullet parity unpinned. */
+#define RIDGE_MAX 2
+#define RIDGE_BREAK 0.02
+#define RIDGE_TOL 1e-5
+#define RIDGE_FLAT 1e-5
+typedef struct { real n[3], d, t; } ridge_hit;
+static int ridge_contacts(const rparams* P, const real* a, const real* b, real r, ridge_hit* out) {
+    real ua = (a[0] - P->hf_o[0]) / P->hf_s[0] + 0.5 * (P->hf_w - 1), ub = (b[0] - P->hf_o[0]) / P->hf_s[0] + 0.5 * (P->hf_w - 1);
+    real va = (a[1] - P->hf_o[1]) / P->hf_s[1] + 0.5 * (P->hf_l - 1), vb = (b[1] - P->hf_o[1]) / P->hf_s[1] + 0.5 * (P->hf_l - 1);
+    if (!(ua > -2 && ua < P->hf_w + 1 && va > -2 && va < P->hf_l + 1 && ub > -2 && ub < P->hf_w + 1 && vb > -2 &&
+          vb < P->hf_l + 1)) return 0;
+    real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    real len = norm3(ab);
+    if (len <= 2 * RIDGE_BREAK) return 0;   /* no interior point clear of both end caps */
+    real reach = r + P->contact_thresh;
+    int i0 = (int)floor((ua < ub ? ua : ub) - reach / P->hf_s[0]), i1 = (int)floor((ua > ub ? ua : ub) + reach / P->hf_s[0]);
+    int j0 = (int)floor((va < vb ? va : vb) - reach / P->hf_s[1]), j1 = (int)floor((va > vb ? va : vb) + reach / P->hf_s[1]);
+    if (i0 < 0) i0 = 0;
+    if (j0 < 0) j0 = 0;
+    if (i1 > P->hf_w - 2) i1 = P->hf_w - 2;
+    if (j1 > P->hf_l - 2) j1 = P->hf_l - 2;
+    int nk = 0;
+    for (int j = j0; j <= j1 + 1; j++)
+        for (int i = i0; i <= i1 + 1; i++)
+            for (int kind = 0; kind < 3; kind++) {
+                /* edge (e0, e1) and the far vertices c1, c2 of its two triangles (diamond subdivision) */
+                int ev[4][2];
+                const int even = !((i + j) & 1);
+                if (kind == 0) {   /* horizontal (i, j)-(i+1, j): cells (i, j-1) and (i, j) */
+                    if (i > i1 || j < 1 || j > P->hf_l - 2) continue;
+                    int e[4][2] = {{i, j}, {i + 1, j}, {even ? i + 1 : i, j + 1}, {even ? i + 1 : i, j - 1}};
+                    memcpy(ev, e, sizeof e);
+                } else if (kind == 1) {   /* vertical (i, j)-(i, j+1): cells (i-1, j) and (i, j) */
+                    if (j > j1 || i < 1 || i > P->hf_w - 2) continue;
+                    int e[4][2] = {{i, j}, {i, j + 1}, {i + 1, even ? j + 1 : j}, {i - 1, even ? j + 1 : j}};
+                    memcpy(ev, e, sizeof e);
+                } else {   /* the diagonal of cell (i, j) */
+                    if (i > i1 || j > j1) continue;
+                    int e[4][2] = {{even ? i : i + 1, j}, {even ? i + 1 : i, j + 1}, {i, even ? j + 1 : j},
+                                   {i + 1, even ? j : j + 1}};
+                    memcpy(ev, e, sizeof e);
+                }
+                real A[3], B[3], C1[3], C2[3], e1[3], f1[3], n1[3], g2[3];
+                hf_vertex(P, ev[0][0], ev[0][1], A);
+                hf_vertex(P, ev[1][0], ev[1][1], B);
+                hf_vertex(P, ev[2][0], ev[2][1], C1);
+                hf_vertex(P, ev[3][0], ev[3][1], C2);
+                for (int k = 0; k < 3; k++) { e1[k] = B[k] - A[k]; f1[k] = C1[k] - A[k]; g2[k] = C2[k] - A[k]; }
+                cross(e1, f1, n1);
+                real conv = dot3(g2, n1);
+                if (n1[2] < 0) conv = -conv;
+                /* flat (to RIDGE_FLAT: float32 height rounding of a planar field) or concave: no interior minimum */
+                if (!(conv < -RIDGE_FLAT * norm3(n1))) continue;
+                real sp[3], ep[3], t, u;
+                seg_seg_st(a, b, A, B, sp, ep, &t, &u);
+                if (!(t * len > RIDGE_BREAK && (1 - t) * len > RIDGE_BREAK)) continue;
+                real dv[3] = {sp[0] - ep[0], sp[1] - ep[1], sp[2] - ep[2]};
+                real dse = norm3(dv);
+                if (!(dse - r < P->contact_thresh)) continue;
+                real n[3], d;
+                if (!terrain_contact(P, sp, r, n, &d)) continue;
+                if (!(d + r < 0 || d + r >= dse - RIDGE_TOL)) continue;   /* a facet is closer: not a minimum */
+                int dup = 0;
+                for (int k = 0; k < nk; k++)
+                    if (fabs(out[k].t - t) * len < RIDGE_BREAK) { dup = 1; break; }
+                if (dup) continue;
+                int slot = nk;
+                if (nk == RIDGE_MAX) {   /* full: replace the shallowest kept if this one is deeper */
+                    slot = out[0].d >= out[1].d ? 0 : 1;
+                    if (!(d < out[slot].d)) continue;
+                } else {
+                    nk++;
+                }
+                for (int k = 0; k < 3; k++) out[slot].n[k] = n[k];
+                out[slot].d = d;
+                out[slot].t = t;
+            }
+    return nk;
+}
+
+static void seg_seg_st(const real* p1, const real* q1, const real* p2, const real* q2, real* c1, real* c2, real* s_out,
+                       real* t_out) {
+    real d1[3], d2[3], r[3];
+    for (int i = 0; i < 3; i++) { d1[i] = q1[i] - p1[i]; d2[i] = q2[i] - p2[i]; r[i] = p1[i] - p2[i]; }
+    real a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    real s, t;
+    const real EPS = 1e-12;
+    if (a <= EPS && e <= EPS) { s = t = 0; }
+    else if (a <= EPS) { s = 0; t = clampd(f / e, 0, 1); }
+    else {
+        real c = dot3(d1, r);
+        if (e <= EPS) { t = 0; s = clampd(-c / a, 0, 1); }
+        else {
+            real b = dot3(d1, d2), den = a * e - b * b;
+            s = (den > EPS) ? clampd((b * f - c * e) / den, 0, 1) : 0;
+            t = (b * s + f) / e;
+            if (t < 0) { t = 0; s = clampd(-c / a, 0, 1); }
+            else if (t > 1) { t = 1; s = clampd((b - c) / a, 0, 1); }
+        }
+    }
+    for (int i = 0; i < 3; i++) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
+    *s_out = s;
+    *t_out = t;
+}
+
 static int collide(const rparams* P, const om_kin* K, om_contact* C) {
     int nc = 0;
     real gp1[OM_NG][3], gp2[OM_NG][3];
@@ -648,6 +775,25 @@ static int collide(const rparams* P, const om_kin* K, om_contact* C) {
                 c->d = d; c->mu = P->mu_ground;
             }
         }
+    }
+    if (P->terrain) {   /* capsule axes across convex terrain edges: slot 0 of every capsule, then slot 1 */
+        ridge_hit rh[OM_NG][RIDGE_MAX];
+        int nr[OM_NG];
+        for (int g = 0; g < OM_NG; g++)
+            nr[g] = om_gtype[g] == 0 ? 0 : ridge_contacts(P, gp1[g], gp2[g], om_gr[g], rh[g]);
+        for (int slot = 0; slot < RIDGE_MAX; slot++)
+            for (int g = 0; g < OM_NG; g++) {
+                if (slot >= nr[g] || nc >= P->max_contacts) continue;
+                const ridge_hit* h = &rh[g][slot];
+                om_contact* c = &C[nc++];
+                c->la = om_glink[g]; c->lb = -1;
+                for (int i = 0; i < 3; i++) {
+                    c->n[i] = h->n[i];
+                    c->pa[i] = gp1[g][i] + h->t * (gp2[g][i] - gp1[g][i]) - om_gr[g] * h->n[i];
+                    c->pb[i] = c->pa[i] - h->d * h->n[i];
+                }
+                c->d = h->d; c->mu = P->mu_ground;
+            }
     }
     if (P->self_collision) {
         for (int k = 0; k < OM_NPAIR; k++) {
@@ -917,5 +1063,19 @@ int om_terrain_contact(const om_params* P, const double* c, double r, double* n,
     rparams Q;
     to_rparams(P, &Q);
     return terrain_contact(&Q, c, r, n, d);
+}
+/* a capsule (axis a-b, radius r) against the heightfield's convex edges: the number of ridge contacts, each
+   out[5 * k ...] = normal (3), signed distance, axis parameter t (tests) */
+int om_ridge_contacts(const om_params* P, const double* a, const double* b, double r, double* out) {
+    rparams Q;
+    to_rparams(P, &Q);
+    ridge_hit h[RIDGE_MAX];
+    int n = ridge_contacts(&Q, a, b, r, h);
+    for (int k = 0; k < n; k++) {
+        for (int i = 0; i < 3; i++) out[5 * k + i] = h[k].n[i];
+        out[5 * k + 3] = h[k].d;
+        out[5 * k + 4] = h[k].t;
+    }
+    return n;
 }
 #endif
