@@ -42,10 +42,14 @@ struct PhysParams {
 
 constexpr int NV = 6 + NDOF;
 // every contact candidate: one per sphere and two per capsule end against the ground plane, plus every
-// non-ancestor geom pair (29 + 66 = 95).  Bullet has no global contact cap, so neither do we: the list
+// non-ancestor geom pair (29 + 66 = 95), plus the heightfield's ridge points (24).  Bullet has no global contact
+// cap, so neither do we: the list
 // holds all of them (max_contacts may lower it for diagnostics; overflow is then flagged)
 constexpr int NCAND_ALL = [] { int n = NPAIR; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 1 : 2; return n; }();
-constexpr int MAXC = NCAND_ALL;         // contact list capacity per substep (ground + self)
+// heightfield ground only (terrain.h ridge_contacts): up to 2 more ground contacts per capsule where its axis
+// crosses a convex terrain edge
+constexpr int NRIDGE_ALL = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 0 : 2; return n; }();
+constexpr int MAXC = NCAND_ALL + NRIDGE_ALL;   // contact list capacity per substep (ground + ridge + self)
 constexpr int ROW_STRIDE = 2 * NV + 6;   // J[NV], MiJ[NV], b, lo, hi, lam, meff, mu
 constexpr int MAX_LIMIT_ROWS = NDOF;     // at most one side of a hinge can be violated
 constexpr int MAXROWS = MAX_LIMIT_ROWS + 3 * MAXC;

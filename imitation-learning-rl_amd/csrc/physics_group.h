@@ -25,7 +25,7 @@ namespace hk {
 constexpr int GL = 16;                       // lanes per env
 // contacts: the first MAXC_LDS of an env's contact list live in LDS, the rest (rare: a lying humanoid with
 // many self contacts) in the env's slice of its block's global spill region; the list holds every candidate
-// (MAXC_G = 29 ground points + 66 geom pairs), so nothing is ever dropped
+// (MAXC_G = 29 ground points + 24 heightfield ridge points + 66 geom pairs), so nothing is ever dropped
 constexpr int MAXC_LDS = 16;
 constexpr int MAXC_G = MAXC;                 // = NCAND_ALL (physics.h)
 constexpr int CW = 12;                       // contact entry: ba, bb, pa[3], pb[3], n[3], d
@@ -237,6 +237,19 @@ constexpr CandDesc cand_desc() {
     return d;
 }
 constexpr CandDesc CDESC = cand_desc();
+// heightfield ground: lane l of an env takes capsule l (geom order) for the ridge contacts (terrain.h)
+constexpr int NCAPS = [] { int n = 0; for (int g = 0; g < NGEOM; g++) n += geom_type[g] == 0 ? 0 : 1; return n; }();
+static_assert(NCAPS <= 16 && NCAPS * RIDGE_MAX + NCAND_GROUND + NPAIR == MAXC, "one capsule per lane; capacity");
+struct CapDesc { unsigned long long c[4]; };
+constexpr CapDesc cap_desc() {
+    CapDesc d{};
+    int l = 0;
+    for (int g = 0; g < NGEOM; g++)
+        if (geom_type[g] != 0) { d.c[l >> 2] |= (unsigned long long)(unsigned)(g | geom_body[g] << 6) << (16 * (l & 3)); l++; }
+    for (; l < 16; l++) d.c[l >> 2] |= 0xffffull << (16 * (l & 3));
+    return d;
+}
+constexpr CapDesc CAPDESC = cap_desc();
 __device__ __attribute__((always_inline)) inline int lane16(int l, unsigned long long c0, unsigned long long c1,
                                                             unsigned long long c2, unsigned long long c3) {
     const int q = l >> 2;
@@ -2032,6 +2045,38 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
                 for (int i = 0; i < 3; i++) pa[i] = p[i] - gr * n[i];
             }
             emit(hit, ba, -1, pa, pa, n, d);
+        }
+        // capsule axes across convex terrain edges (terrain.h ridge_contacts): lane l takes capsule l; slot 0 of every
+        // capsule, then slot 1 (the oracle's order)
+        {
+            const int cd = lane16(lc, CAPDESC.c[0], CAPDESC.c[1], CAPDESC.c[2], CAPDESC.c[3]);
+            T rn[RIDGE_MAX][3], rd[RIDGE_MAX], rt[RIDGE_MAX];
+            int nr = 0;
+            const int ga = cd & 31;
+            if (cd != 0xffff) {
+                const T* p1 = C.gp[ga][0];
+                const T* p2 = C.gp[ga][1];
+                const T aw[3] = {S.st[0] + p1[0], S.st[1] + p1[1], basez + p1[2]};
+                const T bw[3] = {S.st[0] + p2[0], S.st[1] + p2[1], basez + p2[2]};
+                nr = ridge_contacts<T>(P, tkey, aw, bw, gsum[8 * ga + 4], rn, rd, rt);
+            }
+#pragma unroll
+            for (int slot = 0; slot < RIDGE_MAX; slot++) {
+                const bool hit = slot < nr;
+                T pa[3] = {0, 0, 0}, n[3] = {0, 0, 1}, d = 0;
+                if (hit) {
+                    const T* p1 = C.gp[ga][0];
+                    const T* p2 = C.gp[ga][1];
+                    const T gr = gsum[8 * ga + 4];
+#pragma unroll
+                    for (int i = 0; i < 3; i++) {
+                        n[i] = rn[slot][i];
+                        pa[i] = p1[i] + rt[slot] * (p2[i] - p1[i]) - gr * n[i];
+                    }
+                    d = rd[slot];
+                }
+                emit(hit, cd >> 6, -1, pa, pa, n, d);
+            }
         }
     }
     if (P.self_collision) {

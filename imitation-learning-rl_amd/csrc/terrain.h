@@ -6,8 +6,10 @@
 // (i, j) is split along (i,j)-(i+1,j+1) when i + j is even, along (i+1,j)-(i,j+1) otherwise.
 // Contacts (the same sphere / capsule-end candidates as the plane): the closest point of the surface to the
 // candidate's centre over the triangles of the (at most 2 x 2) cells within reach r + contact_thresh; a centre
-// below the plane of the triangle under it takes that triangle's upward normal.  Restated the same way in
-// oracle/physics_oracle.c (terrain_contact).  PyBullet parity unpinned, like the rest of the physics.
+// below the plane of the triangle under it takes that triangle's upward normal.  Capsule bodies additionally touch
+// the terrain's convex edges (ridge_contacts below: the local minima of the axis-to-surface distance inside the
+// axis).  Restated the same way in oracle/physics_oracle.c (terrain_contact, ridge_contacts).  PyBullet parity
+// unpinned, like the rest of the physics.
 #pragma once
 #include "physics.h"
 
@@ -162,6 +164,125 @@ __device__ inline bool terrain_contact(const PhysParams& P, unsigned long long k
         }
     }
     return d < (T)P.contact_thresh;
+}
+
+// closest points of segments p1q1 / p2q2 with their parameters (physics.h seg_seg's clamping, exact divisions)
+template <typename T>
+__device__ inline void seg_seg_st(const T* p1, const T* q1, const T* p2, const T* q2, T* c1, T* c2, T& s, T& t) {
+    T d1[3], d2[3], r[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) { d1[i] = q1[i] - p1[i]; d2[i] = q2[i] - p2[i]; r[i] = p1[i] - p2[i]; }
+    const T a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    const T EPS = (T)1e-12;
+    if (a <= EPS && e <= EPS) { s = t = 0; }
+    else if (a <= EPS) { s = 0; t = clampT(f / e, T(0), T(1)); }
+    else {
+        const T c = dot3(d1, r);
+        if (e <= EPS) { t = 0; s = clampT(-c / a, T(0), T(1)); }
+        else {
+            const T b = dot3(d1, d2), den = a * e - b * b;
+            s = (den > EPS) ? clampT((b * f - c * e) / den, T(0), T(1)) : T(0);
+            t = (b * s + f) / e;
+            if (t < 0) { t = 0; s = clampT(-c / a, T(0), T(1)); }
+            else if (t > 1) { t = 1; s = clampT((b - c) / a, T(0), T(1)); }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
+}
+
+// Capsule bodies against the heightfield (oracle/physics_oracle.c ridge_contacts, where the model is argued):
+// Bullet's convex-concave collision gives a capsule a closest-point contact per triangle under it, kept in one
+// 4-point manifold; restated statelessly as the local minima of the axis-to-surface distance.  Over a facet that
+// distance is linear along the axis and across a concave edge it is the minimum of two linear functions, so the
+// minima are the axis ends (the end-cap candidates above) and the points where the axis passes over a CONVEX edge.
+// For each interior grid edge within reach whose two triangles meet convexly (the far vertex of the second more
+// than RIDGE_FLAT below the first's plane): (s, e) = closest points of axis and edge; kept when s is more than the
+// breaking threshold from both axis ends, when no facet is closer to s than |s - e| - RIDGE_TOL (or s lies inside
+// the terrain), and when terrain_contact at s is in range - the contact is terrain_contact's at s.  A candidate within
+// the breaking threshold of a kept one is dropped; at most RIDGE_MAX per capsule (with the two end caps, Bullet's
+// 4-point manifold), a deeper one replacing the shallowest kept.  Edge walk: vertex rows j, vertices i, then the
+// horizontal, vertical and diagonal edge anchored at vertex (i, j).  Returns the count; per kept contact the normal,
+// signed distance and axis parameter t.
+constexpr int RIDGE_MAX = 2;
+template <typename T>
+__device__ inline int ridge_contacts(const PhysParams& P, unsigned long long key, const T* a, const T* b, T r,
+                                     T (*rn)[3], T* rd, T* rt) {
+    const T RIDGE_BREAK = (T)0.02, RIDGE_TOL = (T)1e-5, RIDGE_FLAT = (T)1e-5;
+    const T sx = (T)P.hf_s[0], sy = (T)P.hf_s[1], cw = (T)(0.5 * (P.hf_w - 1)), cl = (T)(0.5 * (P.hf_l - 1));
+    const T ua = (a[0] - (T)P.hf_o[0]) / sx + cw, ub = (b[0] - (T)P.hf_o[0]) / sx + cw;
+    const T va = (a[1] - (T)P.hf_o[1]) / sy + cl, vb = (b[1] - (T)P.hf_o[1]) / sy + cl;
+    if (!(ua > T(-2) && ua < (T)(P.hf_w + 1) && va > T(-2) && va < (T)(P.hf_l + 1) && ub > T(-2) &&
+          ub < (T)(P.hf_w + 1) && vb > T(-2) && vb < (T)(P.hf_l + 1))) return 0;
+    T ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    const T len = sqrt(dot3(ab, ab));
+    if (len <= T(2) * RIDGE_BREAK) return 0;
+    const T reach = r + (T)P.contact_thresh;
+    int i0 = (int)floor((ua < ub ? ua : ub) - reach / sx), i1 = (int)floor((ua > ub ? ua : ub) + reach / sx);
+    int j0 = (int)floor((va < vb ? va : vb) - reach / sy), j1 = (int)floor((va > vb ? va : vb) + reach / sy);
+    i0 = i0 < 0 ? 0 : i0;
+    j0 = j0 < 0 ? 0 : j0;
+    i1 = i1 > P.hf_w - 2 ? P.hf_w - 2 : i1;
+    j1 = j1 > P.hf_l - 2 ? P.hf_l - 2 : j1;
+    int nk = 0;
+#pragma unroll 1
+    for (int j = j0; j <= j1 + 1; j++)
+#pragma unroll 1
+        for (int i = i0; i <= i1 + 1; i++)
+#pragma unroll 1
+            for (int kind = 0; kind < 3; kind++) {
+                const bool even = !((i + j) & 1);
+                int ev[4][2];   // edge (0, 1) and the far vertices of its two triangles (diamond subdivision)
+                if (kind == 0) {   // horizontal (i, j)-(i+1, j): cells (i, j-1) and (i, j)
+                    if (i > i1 || j < 1 || j > P.hf_l - 2) continue;
+                    ev[0][0] = i; ev[0][1] = j; ev[1][0] = i + 1; ev[1][1] = j;
+                    ev[2][0] = even ? i + 1 : i; ev[2][1] = j + 1; ev[3][0] = even ? i + 1 : i; ev[3][1] = j - 1;
+                } else if (kind == 1) {   // vertical (i, j)-(i, j+1): cells (i-1, j) and (i, j)
+                    if (j > j1 || i < 1 || i > P.hf_w - 2) continue;
+                    ev[0][0] = i; ev[0][1] = j; ev[1][0] = i; ev[1][1] = j + 1;
+                    ev[2][0] = i + 1; ev[2][1] = even ? j + 1 : j; ev[3][0] = i - 1; ev[3][1] = even ? j + 1 : j;
+                } else {   // the diagonal of cell (i, j)
+                    if (i > i1 || j > j1) continue;
+                    ev[0][0] = even ? i : i + 1; ev[0][1] = j; ev[1][0] = even ? i + 1 : i; ev[1][1] = j + 1;
+                    ev[2][0] = i; ev[2][1] = even ? j + 1 : j; ev[3][0] = i + 1; ev[3][1] = even ? j : j + 1;
+                }
+                T A[3], B[3], C1[3], C2[3], e1[3], f1[3], g2[3], n1[3];
+                terrain_vertex(P, key, ev[0][0], ev[0][1], A);
+                terrain_vertex(P, key, ev[1][0], ev[1][1], B);
+                terrain_vertex(P, key, ev[2][0], ev[2][1], C1);
+                terrain_vertex(P, key, ev[3][0], ev[3][1], C2);
+#pragma unroll
+                for (int k = 0; k < 3; k++) { e1[k] = B[k] - A[k]; f1[k] = C1[k] - A[k]; g2[k] = C2[k] - A[k]; }
+                cross3(e1, f1, n1);
+                T conv = dot3(g2, n1);
+                if (n1[2] < T(0)) conv = -conv;
+                if (!(conv < -RIDGE_FLAT * sqrt(dot3(n1, n1)))) continue;   // flat or concave
+                T sp[3], ep[3], t, u;
+                seg_seg_st(a, b, A, B, sp, ep, t, u);
+                if (!(t * len > RIDGE_BREAK && (T(1) - t) * len > RIDGE_BREAK)) continue;
+                const T dv[3] = {sp[0] - ep[0], sp[1] - ep[1], sp[2] - ep[2]};
+                const T dse = sqrt(dot3(dv, dv));
+                if (!(dse - r < (T)P.contact_thresh)) continue;
+                T n[3], d;
+                if (!terrain_contact<T>(P, key, sp, r, n, d)) continue;
+                if (!(d + r < T(0) || d + r >= dse - RIDGE_TOL)) continue;   // a facet is closer: not a minimum
+                bool dup = false;
+                for (int k = 0; k < nk; k++)
+                    if (fabs(rt[k] - t) * len < RIDGE_BREAK) dup = true;
+                if (dup) continue;
+                int slot = nk;
+                if (nk == RIDGE_MAX) {
+                    slot = rd[0] >= rd[1] ? 0 : 1;
+                    if (!(d < rd[slot])) continue;
+                } else {
+                    nk++;
+                }
+#pragma unroll
+                for (int k = 0; k < 3; k++) rn[slot][k] = n[k];
+                rd[slot] = d;
+                rt[slot] = t;
+            }
+    return nk;
 }
 
 }  // namespace hk

@@ -13,10 +13,11 @@ LIB_PATH = os.environ.get("ILRL_AMD_LIB", DEFAULT_LIB_PATH)
 # signatures are unchanged - later ones only added entry points).  Without it every library, override or not,
 # must match HUM_ABI_VERSION and export every symbol.
 AB_MODE = os.environ.get("ILRL_AMD_AB") == "1"
-AB_COMPATIBLE_ABIS = (8, 9, 10, 11, 12)   # ABI 10 added hum_policy_create_ex, hum_hier_rollout; 11 hum_pack_rows;
-# 12 hum_hier_rollout_fused; 13 hum_rollout_fused_ex, hum_hier_rollout_fused_ex (the policy mean traces)
+AB_COMPATIBLE_ABIS = (8, 9, 10, 11, 12, 13)   # ABI 10 added hum_policy_create_ex, hum_hier_rollout; 11 hum_pack_rows;
+# 12 hum_hier_rollout_fused; 13 hum_rollout_fused_ex, hum_hier_rollout_fused_ex (the policy mean traces); 14 the
+# heightfield ridge contacts (HUM_MAX_CONTACTS 95 -> 119) and the IPC fragment transport
 
-HUM_ABI_VERSION = 13   # include/humanoid_env.h
+HUM_ABI_VERSION = 14   # include/humanoid_env.h
 HUM_NSTATE, HUM_NOBS, HUM_NACT, HUM_NBOOK, HUM_NAUX = 47, 70, 17, 48, 17
 HUM_NOBS_HIGH, HUM_NACT_HIGH = 44, 2
 HUM_AGENT_HIGH, HUM_AGENT_LOW, HUM_AGENT_SEL_SKIP = 1, 2, 255
@@ -26,7 +27,7 @@ HUM_EFLAG_NONFINITE_ACTION, HUM_EFLAG_VEL_ROW, HUM_EFLAG_CONTACT_OVERFLOW, HUM_E
 HUM_EFLAG_DIAG_BOUNDS = 0x80000000   # bounds-checked diagnostic builds only (-DHUM_BOUNDS_CHECK)
 HUM_NUMPY_1, HUM_NUMPY_2 = 1, 2
 HUM_RESET_NO_REF_POSE, HUM_RESET_NO_INIT_VEL = 1, 2
-HUM_MAX_CONTACTS = 95
+HUM_MAX_CONTACTS = 119
 HUM_TERRAIN_PLANE, HUM_TERRAIN_HEIGHTFIELD, HUM_TERRAIN_RANDOM_BLOCKS = 0, 1, 2
 HUM_OK, HUM_ERR_ARG, HUM_ERR_HIP, HUM_ERR_NOCLIP, HUM_ERR_STATE = 0, -1, -2, -3, -4
 

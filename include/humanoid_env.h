@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HUM_ABI_VERSION 13
+#define HUM_ABI_VERSION 14
 #define HUM_NSTATE 47   /* physics state per lane */
 #define HUM_NOBS 70     /* observation_space shape, low_level_env.py:53-55 */
 #define HUM_NACT 17     /* action_space shape, low_level_env.py:56 */
@@ -44,7 +44,8 @@ extern "C" {
 #define HUM_NACT_HIGH 2    /* high_level_act_space shape (cos, sin of the heading), hier_env.py:53-55 */
 #define HUM_NAUX 17     /* RewardLogCallback terms + calcEndPointScore + robot_pos per lane, HUM_AUX_* below */
 #define HUM_MAX_CLIPS 8
-#define HUM_MAX_CONTACTS 95  /* every contact candidate: 29 sphere / capsule-end ground points + 66 geom pairs */
+#define HUM_MAX_CONTACTS 119  /* every contact candidate: 29 sphere / capsule-end ground points, 24 heightfield ridge
+                                points (2 per capsule, ABI 14), 66 geom pairs */
 
 /* status codes */
 #define HUM_OK 0

@@ -177,6 +177,15 @@ def ridge_contacts(a, b, r, params):
     return [(out[5 * k:5 * k + 3].copy(), float(out[5 * k + 3]), float(out[5 * k + 4])) for k in range(n)]
 
 
+def geom_segments(state):
+    """[17, 8]: every geom's world segment p1, p2, radius, type (0 sphere, 1 capsule)."""
+    out = np.zeros((17, 8))
+    f = lib().om_geom_segments
+    f.argtypes = [ctypes.POINTER(ctypes.c_double)] * 2
+    f(_p(np.ascontiguousarray(state, dtype=np.float64)), _p(out))
+    return out
+
+
 def parts(state):
     out = np.zeros((33, 3))
     st = np.ascontiguousarray(state, dtype=np.float64)

@@ -1064,6 +1064,17 @@ int om_terrain_contact(const om_params* P, const double* c, double r, double* n,
     to_rparams(P, &Q);
     return terrain_contact(&Q, c, r, n, d);
 }
+/* every geom's world segment: out[8 * g ...] = p1 (3), p2 (3), radius, type (0 sphere, 1 capsule) (tests) */
+void om_geom_segments(const double* st, double* out) {
+    om_kin K;
+    fk(st, &K);
+    for (int g = 0; g < OM_NG; g++) {
+        link_point(&K, om_glink[g], om_gp1 + 3 * g, out + 8 * g);
+        link_point(&K, om_glink[g], om_gp2 + 3 * g, out + 8 * g + 3);
+        out[8 * g + 6] = om_gr[g];
+        out[8 * g + 7] = om_gtype[g] == 0 ? 0 : 1;
+    }
+}
 /* a capsule (axis a-b, radius r) against the heightfield's convex edges: the number of ridge contacts, each
    out[5 * k ...] = normal (3), signed distance, axis parameter t (tests) */
 int om_ridge_contacts(const om_params* P, const double* a, const double* b, double r, double* out) {

@@ -76,7 +76,7 @@ def test_hier_rollout_struct_layouts_match_header(tmp_path, cname, cls):
 def test_default_config_values():
     c = N.default_config()
     assert (c.dt_env, c.substeps, c.solver_iters, c.gravity) == (0.0165, 4, 5, 9.8)
-    assert abs(c.mu_ground - 1.6) < 1e-15 and c.erp_contact == 0.9 and c.max_contacts == 95 and c.kernel == 1
+    assert abs(c.mu_ground - 1.6) < 1e-15 and c.erp_contact == 0.9 and c.max_contacts == 119 and c.kernel == 1
     P = O.default_params()
     assert P.max_contacts == c.max_contacts and P.erp_limit == c.erp_limit and P.contact_thresh == c.contact_thresh
     assert P.limit_max_impulse == c.limit_max_impulse and P.max_coord_vel == c.max_coord_vel

@@ -195,3 +195,67 @@ def test_custom_env_view():
     env.close()
     with pytest.raises(N.NativeError):
         HumanoidVecEnv(4, clips=(CLIP,), kernel=0).set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
+
+
+def _ridge_states(keys, terrain, seed=11, need=1):
+    """per lane (its terrain key): a random humanoid pose placed over CustomScene's random blocks so that at least
+    `need` capsule axes cross a convex block edge within contact range (oracle ridge_contacts), with the number of
+    ridge contacts per lane"""
+    rng = np.random.default_rng(seed)
+    from scipy.spatial.transform import Rotation as R
+    out, counts = [], []
+    for key in keys:
+        P = terrain.apply(O.default_params(), int(key))
+        while True:
+            st = np.zeros(O.NSTATE)
+            st[3:7] = R.random(random_state=int(rng.integers(1 << 30))).as_quat()
+            st[13:30] = rng.uniform(O.LO, O.HI)
+            st[0:2] = rng.uniform(-20, 20, 2)
+            st[2] = -O.parts(st)[:32, 2].min()
+            x, y = st[0], st[1]
+            hs = [float(O.random_block_height(int(key), (int(np.floor(x + 127.5)) + di) >> 1,
+                                              (int(np.floor(y + 127.5)) + dj) >> 1))
+                  for di in (-1, 0, 1, 2) for dj in (-1, 0, 1, 2)]
+            st[2] += max(hs) - terrain.mid + terrain.origin[2] + rng.uniform(-0.06, 0.0)
+            st[7:13] = rng.uniform(-0.5, 0.5, 6)
+            segs = O.geom_segments(st)
+            nr = sum(len(O.ridge_contacts(segs[g, :3], segs[g, 3:6], segs[g, 6], P)) for g in range(17) if segs[g, 7])
+            if nr >= need:
+                out.append(st)
+                counts.append(nr)
+                break
+    return np.array(out), np.array(counts)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_limbs_across_block_edges_match_oracle(precision):
+    """Capsule bodies against the heightfield (csrc/terrain.h ridge_contacts vs oracle/physics_oracle.c): every lane
+    starts from a pose whose limbs cross a raised block's convex edge within contact range (1-4 ridge contacts per
+    lane besides the end caps), and one env step of the GPU kernel matches the oracle's physics from the identical
+    state.  fp64: state <= 1e-10 (the same algorithm in two exact formulations); fp32: FP32_TERRAIN_BOUND on obs."""
+    n = 64
+    clip = load_clip(CLIP)
+    terrain = O.Terrain(O.TERRAIN_RANDOM_BLOCKS)
+    env = HumanoidVecEnv(n, clips=(CLIP,), seed=21, precision=precision)
+    env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
+    env.reset()
+    _, book = env.get_state()
+    keys = [int(book[k, BK["terrain_key_lo"]]) | (int(book[k, BK["terrain_key_hi"]]) << 32) for k in range(n)]
+    states, counts = _ridge_states(keys, terrain)
+    assert counts.sum() >= n
+    env.set_state(states, book)
+    a = np.random.default_rng(4).uniform(-1, 1, (n, 17)).astype(np.float32)
+    if precision == "fp64":
+        env.step(torch.as_tensor(a, device="cuda"))
+        phys, _ = env.get_state()
+        assert env.error_flags() & N.HUM_EFLAG_CONTACT_OVERFLOW == 0
+        errs = []
+        for i in range(n):
+            ref = O.phys_step(states[i], O.motor_torques(a[i]), terrain.apply(O.default_params(), keys[i]))
+            errs.append(np.abs(phys[i] - ref).max())
+        print("ridge lanes fp64: state max %.3g (ridge contacts per lane %d..%d)" % (max(errs), counts.min(), counts.max()))
+        assert max(errs) < 1e-10, max(errs)
+    else:
+        res = _one_step_vs_oracle(env, terrain, a, clip)
+        _check(res, precision)
+    env.close()
