@@ -75,6 +75,11 @@ def parse():
                          "columns RLlib's sampler records - action_dist_inputs, action_logp and vf_preds from a "
                          "value branch of the same shape (random-init) - over the launch's rows")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / parity side measurements")
+    ap.add_argument("--adapter", action="store_true",
+                    help="time the RLlib drop-in path instead of the raw C-ABI launches: HumanoidVectorEnv.vector_step + "
+                         "reset_at per done lane (RLlib 1.2 VectorEnv), or with --hier HierarchicalVectorEnv.poll / "
+                         "send_actions / try_reset (BaseEnv); host-side numpy actions as RLlib hands them over, one launch "
+                         "per sampler step (k = 1)")
     return ap.parse_args()
 
 
@@ -423,6 +428,91 @@ def count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank):
     return low
 
 
+def run_adapter(a, dev, n):
+    """The path a reference user's RLlib sampler drives (train_config.py:13-29,320-321): per sampler step the
+    policy's actions arrive as host numpy rows, one env launch runs, and the results go back as per-env Python
+    objects; done envs are then reset through reset_at / try_reset (served from the launch's auto-reset rows).
+    Actions are pre-drawn host arrays (the policy is RLlib's, outside this path); everything the adapter does -
+    the action upload, the launch, the copies back, the per-env lists / dicts, the resets - is timed."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(1234)
+    steps, warm = a.steps, a.warmup
+    t_adapter = 0.0
+    if not a.hier:
+        from ilrl_amd.low_level_env import HumanoidVectorEnv
+        venv = HumanoidVectorEnv(n, reference_name=a.clip, seed=0, device=dev.index)
+        pool = [list(rng.uniform(-1, 1, (n, 17)).astype(np.float32)) for _ in range(16)]   # RLlib: a list of rows
+        venv.vector_reset()
+        phys_steps, resets = 0, 0
+
+        def step(s):
+            nonlocal resets
+            obs, rew, done, info = venv.vector_step(pool[s % 16])
+            for i in np.flatnonzero(done):
+                venv.reset_at(int(i))
+                resets += 1
+            return n
+        for w in range(warm):
+            step(w)
+        resets = 0
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for s in range(steps):
+            phys_steps += step(s)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        env = venv.venv
+        desc = "HumanoidVectorEnv.vector_step (RLlib 1.2 VectorEnv) + reset_at per done env"
+        transitions = phys_steps
+    else:
+        from ilrl_amd.hier_env import HIGH, LOW, HierarchicalVectorEnv
+        venv = HierarchicalVectorEnv(n, seed=0, device=dev.index)
+        hp = [rng.uniform(-1, 1, (n, 2)).astype(np.float32) for _ in range(16)]
+        lp = [rng.uniform(-1, 1, (n, 17)).astype(np.float32) for _ in range(16)]
+        phys_steps = transitions = resets = 0
+        t_dict = [0.0]
+
+        def step(s):   # RLlib 1.2's sampler: poll, reset the done envs, act on every returned agent obs
+            nonlocal phys_steps, transitions, resets
+            obs, rew, dones, infos, _ = venv.poll()
+            for i, d in dones.items():
+                if d["__all__"]:
+                    obs[i] = venv.try_reset(i)
+                    resets += 1
+            th = time.perf_counter()
+            acts, h, l = {}, hp[s % 16], lp[s % 16]
+            for i, ob in obs.items():   # the policy's output, one dict per acting agent (RLlib's work, not the adapter's)
+                acts[i] = {HIGH: h[i]} if HIGH in ob else {LOW: l[i]}
+            nlow = sum(1 for ad in acts.values() if LOW in ad)
+            t_dict[0] += time.perf_counter() - th
+            venv.send_actions(acts)
+            phys_steps += nlow
+            transitions += len(acts)
+        for w in range(warm):
+            step(w)
+        torch.cuda.synchronize(dev)
+        t_dict[0] = 0.0
+        phys_steps = transitions = resets = 0
+        t0 = time.perf_counter()
+        for s in range(steps):
+            step(s)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0 - t_dict[0]
+        env = venv.venv
+        desc = ("HierarchicalVectorEnv.poll / send_actions / try_reset (RLlib 1.2 BaseEnv); the harness's per-env "
+                "action dicts (RLlib's work) excluded: %.4f s" % t_dict[0])
+    out = {"metric": "env steps/sec at N parallel humanoids, 1/2/4/8 MI355X; obs/reward max-abs-err vs PyBullet",
+           "value": phys_steps / wall, "unit": "env-steps/s", "n_gpus": 1, "steps": steps, "warmup": warm,
+           "ms_per_step": wall / steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": a.precision.replace("fp", "f"), "data": "synthetic",
+           "config": {"workload": "RLlib drop-in adapter: %s, %s, %d envs, uniform random host actions, k = 1" % (
+               desc, a.clip, n), "adapter": True, "envs_per_gpu": n, "clip": a.clip, "hier": bool(a.hier)},
+           "resets": resets, "agent_transitions_per_s": transitions / wall, "error_flags": env.error_flags()}
+    print(json.dumps(out), flush=True)
+    venv.stop() if a.hier else venv.venv.close()
+
+
 def main():
     a = parse()
     import torch
@@ -458,6 +548,8 @@ def main():
         a.k = 1   # closed loop: the policy acts on every step's observation, one launch each
     if a.k < 1:
         raise SystemExit("--k must be >= 1")
+    if a.adapter:
+        return run_adapter(a, dev, n)
     if a.gather_every is None:
         a.gather_every = a.k if world > 1 and not a.policy else 0
     env, wall_max, kern_ms, low_steps, gather_s, gathered, sizes = run(a, world, rank, dev, n, a.precision, a.steps,
