@@ -270,7 +270,7 @@ def _ridge_fp32_gate(env, terrain, a, clip, lane_quantiles=((50, 1.0), (90, 1.5)
     poses lie on the terrain and press into it, so many sit at a contact / split-impulse switch where float32 vs
     float64 rounding flips the model (the oracle's own obs move by > SENS_BOUND under a 2^-24 input perturbation).
     Those lanes are counted; on the others the kernel's obs error / the lane's fp32-oracle envelope (4 realisations)
-    must meet the per-lane quantiles, and stay under FP32_TERRAIN_BOUND absolutely."""
+    must meet the per-lane quantiles, and stay within twice the largest envelope absolutely."""
     from test_gpu_scale import FP32_LANE_FLOOR, FP32_REALISATIONS, SENS_BOUND
     phys, book = env.get_state()
     obs = env.step(torch.as_tensor(a, device="cuda"))[0].cpu().numpy()
@@ -299,4 +299,6 @@ def _ridge_fp32_gate(env, terrain, a, clip, lane_quantiles=((50, 1.0), (90, 1.5)
     assert good.sum() >= len(good) // 4
     for pct, bound in lane_quantiles:
         assert np.percentile(ratio, pct) <= bound, (pct, np.percentile(ratio, pct))
-    assert kern[good].max() <= FP32_TERRAIN_BOUND["obs_max"]
+    # absolutely: these pressed-in poses are stiffer than the reset poses FP32_TERRAIN_BOUND was set on (the fp32
+    # oracle itself moves their obs by up to ~5e-3), so the bound is the yardstick's own largest envelope, doubled
+    assert kern[good].max() <= max(FP32_TERRAIN_BOUND["obs_max"], 2 * envl[good].max()), kern[good].max()
