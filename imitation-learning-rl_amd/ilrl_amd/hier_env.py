@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _native as N
 from .low_level_env import _box, _BookView, _optional_base, env_seed
-from .vec_env import HumanoidVecEnv, _ptr
+from .vec_env import HostStaging, HumanoidVecEnv, _ptr
 
 ENV_HIER = "HumanoidBulletEnv-v0-Hier"
 HIGH, LOW = "high_level_agent", "low_level_agent"
@@ -235,8 +235,14 @@ class HierarchicalVectorEnv(_optional_base("ray.rllib.env.base_env", "BaseEnv"))
         self._views = [HierLaneView(self, i) for i in range(num_envs)]
         self._book_cache = None
         self._pending = None
-        self._reset_obs = None
-        self._reset_pending = np.zeros(num_envs, dtype=bool)
+        self._reset_rows = {}
+        self._io = HostStaging(self.venv.torch, self.venv.device)
+        t = self.venv.torch
+        self._ah = np.zeros((num_envs, 2), np.float32)   # host staging of the per-env actions (rows of skipped
+        self._al = np.zeros((num_envs, 17), np.float32)  # lanes / the other agent are never read by the kernel)
+        self._dev = {"ah": t.empty(num_envs, 2, dtype=t.float32, device=self.venv.device),
+                     "al": t.empty(num_envs, 17, dtype=t.float32, device=self.venv.device),
+                     "ag": t.empty(num_envs, dtype=t.uint8, device=self.venv.device)}
 
     def _books(self):
         if self._book_cache is None:
@@ -259,42 +265,68 @@ class HierarchicalVectorEnv(_optional_base("ray.rllib.env.base_env", "BaseEnv"))
         return obs, rew, dones, infos, {}
 
     def send_actions(self, action_dict):
-        """Lanes absent from action_dict (RLlib did not act on them) are left unstepped (HUM_AGENT_SEL_SKIP)."""
+        """Lanes absent from action_dict (RLlib did not act on them) are left unstepped (HUM_AGENT_SEL_SKIP).
+        One pass over the per-env dicts sorts the actions by agent; they go up through pinned buffers, one launch
+        runs, and every output comes back in one synchronize (the done lanes' reset rows in a second, only when a
+        lane is done); the per-env result dicts are built from whole-array conversions."""
         n = self.num_envs
-        ah = np.zeros((n, 2), np.float32)
-        al = np.zeros((n, 17), np.float32)
-        agent = np.full(n, N.HUM_AGENT_SEL_SKIP, np.uint8)
+        hi_ids, hi_rows, lo_ids, lo_rows = [], [], [], []
         for i, ad in action_dict.items():
-            assert len(ad) == 1, ad
-            if HIGH in ad:
-                ah[i] = ad[HIGH]
-                agent[i] = 1
-            else:
-                al[i] = list(ad.values())[0]
-                agent[i] = 0
-        if not np.isfinite(al).all():
-            raise AssertionError("non-finite action (humanoid.py:55)")
-        agents, oh, ol, rh, rl, done, _ = [x.cpu().numpy() for x in
-                                           self.venv.step(ah, al, agent=agent, autoreset=True)]
-        self._reset_obs = self.venv.obs_high_reset.cpu().numpy().astype(np.float64)
-        self._reset_pending = done.astype(bool).copy()
+            if len(ad) != 1:
+                raise AssertionError(ad)
+            for agent_id, act in ad.items():
+                if agent_id == HIGH:
+                    hi_ids.append(i)
+                    hi_rows.append(act)
+                else:
+                    lo_ids.append(i)
+                    lo_rows.append(act)
+        agent = np.full(n, N.HUM_AGENT_SEL_SKIP, np.uint8)
+        if hi_ids:
+            self._ah[hi_ids] = np.asarray(hi_rows, dtype=np.float32).reshape(len(hi_ids), 2)
+            agent[hi_ids] = 1
+        if lo_ids:
+            lo = np.asarray(lo_rows, dtype=np.float32).reshape(len(lo_ids), 17)
+            if not np.isfinite(lo).all():
+                raise AssertionError("non-finite action (humanoid.py:55)")
+            self._al[lo_ids] = lo
+            agent[lo_ids] = 0
+        io, d, v = self._io, self._dev, self.venv
+        out = v.step(io.upload("ah", self._ah, d["ah"]), io.upload("al", self._al, d["al"]),
+                     agent=io.upload("ag", agent, d["ag"]), autoreset=True)
+        agents, oh, ol, rh, rl, done, _ = out
+        h = io.fetch(agents=agents, oh=oh, ol=ol, rh=rh, rl=rl, done=done)
+        oh64, ol64 = h["oh"].astype(np.float64), h["ol"].astype(np.float64)   # the reference's float64 obs
+        ag, rhl, rll, dn = h["agents"].tolist(), h["rh"].tolist(), h["rl"].tolist(), h["done"].astype(bool).tolist()
+        self._reset_rows = {}
+        idx = np.flatnonzero(h["done"])
+        if idx.size:   # the done lanes' auto-reset high-level observations only (try_reset serves them)
+            rows = io.fetch_rows("reset", v.obs_high_reset.index_select(0, v.torch.from_numpy(idx).to(v.device)),
+                                 n).astype(np.float64)
+            self._reset_rows = dict(zip(idx.tolist(), rows))
         self._book_cache = None
+        AH, AL = N.HUM_AGENT_HIGH, N.HUM_AGENT_LOW
         obs, rew, dones, infos = {}, {}, {}, {}
         for i in action_dict:
-            o, r = {}, {}
-            if agents[i] & N.HUM_AGENT_HIGH:
-                o[HIGH] = oh[i].astype(np.float64)
-                r[HIGH] = float(rh[i])
-            if agents[i] & N.HUM_AGENT_LOW:
-                o[LOW] = ol[i].astype(np.float64)
-                r[LOW] = float(rl[i])
-            obs[i], rew[i], dones[i], infos[i] = o, r, {"__all__": bool(done[i])}, {k: {} for k in o}
+            a = ag[i]
+            if a == AH:
+                obs[i], rew[i], infos[i] = {HIGH: oh64[i]}, {HIGH: rhl[i]}, {HIGH: {}}
+            elif a == AL:
+                obs[i], rew[i], infos[i] = {LOW: ol64[i]}, {LOW: rll[i]}, {LOW: {}}
+            else:   # both agents report (the level hand-back, or done)
+                o, r = {}, {}
+                if a & AH:
+                    o[HIGH], r[HIGH] = oh64[i], rhl[i]
+                if a & AL:
+                    o[LOW], r[LOW] = ol64[i], rll[i]
+                obs[i], rew[i], infos[i] = o, r, {k: {} for k in o}
+            dones[i] = {"__all__": dn[i]}
         self._pending = (obs, rew, dones, infos)
 
     def try_reset(self, env_id):
-        if self._reset_pending[env_id]:
-            self._reset_pending[env_id] = False
-            return {HIGH: self._reset_obs[env_id]}
+        row = self._reset_rows.pop(env_id, None)
+        if row is not None:
+            return {HIGH: row}
         mask = np.zeros(self.num_envs, dtype=np.uint8)
         mask[env_id] = 1
         self._book_cache = None
@@ -321,8 +353,10 @@ def make_env_hier_vec(env_config=None):
     return HierarchicalVectorEnv(n, seed=seed, lane_offset=off)
 
 
-def register_envs():
-    """register_env(ENV_HIER, make_env_hier) (train_config.py:320) when Ray is importable."""
+def register_envs(vectorised=True):
+    """register_env(ENV_HIER, ...) (train_config.py:320) when Ray is importable: the N-lane BaseEnv per worker
+    (default, make_env_hier_vec: one launch per sampler step for all of the worker's envs), or the reference's
+    one-env-per-call creator (make_env_hier: one handle and one launch per env)."""
     from ray.tune.registry import register_env
-    register_env(ENV_HIER, make_env_hier)
+    register_env(ENV_HIER, make_env_hier_vec if vectorised else make_env_hier)
     return ENV_HIER

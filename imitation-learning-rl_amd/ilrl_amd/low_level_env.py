@@ -20,7 +20,7 @@ import secrets
 import numpy as np
 
 from . import _native as N
-from .vec_env import HumanoidVecEnv
+from .vec_env import HostStaging, HumanoidVecEnv
 
 ENV_LOW = "HumanoidBulletEnv-v0-Low"
 
@@ -280,7 +280,9 @@ class HumanoidVectorEnv(_optional_base("ray.rllib.env.vector_env", "VectorEnv"))
             super().__init__(self.observation_space, self.action_space, num_envs)
         self._book_cache = None
         self._aux_rows = {}
-        self._reset_obs = None
+        self._reset_rows = {}
+        self._act_dev = None
+        self._io = None
         self._views = [LaneView(self, i) for i in range(num_envs)]
 
     def _books(self):
@@ -302,12 +304,13 @@ class HumanoidVectorEnv(_optional_base("ray.rllib.env.vector_env", "VectorEnv"))
     def vector_reset(self):
         obs = self.venv.reset().cpu().numpy()
         self._invalidate()
-        return [o for o in obs]
+        self._reset_rows = {}
+        return list(obs)
 
     def reset_at(self, index):
-        if self._reset_obs is not None and self._reset_pending[index]:
-            self._reset_pending[index] = False
-            return self._reset_obs[index]
+        row = self._reset_rows.pop(index, None)
+        if row is not None:   # the auto-reset observation the step launch already produced for this lane
+            return row
         mask = np.zeros(self.num_envs, dtype=np.uint8)
         mask[index] = 1
         obs = self.venv.reset(mask=mask)[index].cpu().numpy()
@@ -315,15 +318,30 @@ class HumanoidVectorEnv(_optional_base("ray.rllib.env.vector_env", "VectorEnv"))
         return obs
 
     def vector_step(self, actions):
-        a = np.asarray(actions, dtype=np.float32).reshape(self.num_envs, 17)
+        """One launch for every lane.  Host work is kept to what the VectorEnv API needs: the actions (RLlib hands a
+        list of per-env rows) are stacked once and uploaded through a pinned buffer; obs / reward / done come back
+        through pinned buffers with one stream synchronize; only the done lanes' auto-reset rows are fetched
+        (reset_at serves them); rewards and dones become Python lists in one call each."""
+        a = actions if isinstance(actions, np.ndarray) else np.concatenate(actions)
+        a = np.asarray(a, dtype=np.float32).reshape(self.num_envs, 17)
         if not np.isfinite(a).all():   # humanoid.py:55, checked on the host copy RLlib hands over (no device sync)
             raise AssertionError("non-finite action (humanoid.py:55)")
-        obs, rew, done, _ = self.venv.step(a, autoreset=True)
-        o, r, d = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy().astype(bool)
-        self._reset_obs = self.venv.obs_reset.cpu().numpy()
-        self._reset_pending = d.copy()
+        v = self.venv
+        if self._act_dev is None:
+            self._act_dev = v.torch.empty(self.num_envs, 17, dtype=v.torch.float32, device=v.device)
+            self._io = HostStaging(v.torch, v.device)
+        obs, rew, done, _ = v.step(self._io.upload("act", a, self._act_dev), autoreset=True)
+        h = self._io.fetch(obs=obs, rew=rew, done=done)
+        o = h["obs"].copy()   # the rows handed out outlive the pinned buffer
+        d = h["done"].astype(bool)
+        self._reset_rows = {}
+        idx = np.flatnonzero(d)
+        if idx.size:   # the done lanes' auto-reset observations only (reset_at serves them)
+            rows = self._io.fetch_rows("reset", v.obs_reset.index_select(0, v.torch.from_numpy(idx).to(v.device)),
+                                       self.num_envs).copy()
+            self._reset_rows = dict(zip(idx.tolist(), rows))
         self._invalidate()
-        return [x for x in o], [float(x) for x in r], [bool(x) for x in d], [{} for _ in range(self.num_envs)]
+        return list(o), h["rew"].tolist(), d.tolist(), [{} for _ in range(self.num_envs)]
 
     def get_unwrapped(self):
         return self._views

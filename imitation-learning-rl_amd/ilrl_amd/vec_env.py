@@ -20,6 +20,48 @@ def _dp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
+class HostStaging:
+    """Pinned host buffers for the drop-in adapters (one per slot name): device tensors are copied into them with
+    non_blocking copies on the launch stream and ONE stream synchronize waits for all of them (a pageable .cpu() per
+    tensor is one blocking round trip each).  The numpy views returned stay valid until that slot's next fetch;
+    callers copy what they hand out.  `upload` stages a host array into a device tensor the same way (the next
+    fetch's synchronize also retires the upload before the pinned buffer is reused)."""
+
+    def __init__(self, torch, device):
+        self.torch, self.device, self.buf = torch, device, {}
+
+    def _pinned(self, name, shape, dtype):
+        b = self.buf.get(name)
+        if b is None or tuple(b.shape) != tuple(shape) or b.dtype != dtype:
+            b = self.torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
+            self.buf[name] = b
+        return b
+
+    def fetch(self, **xs):
+        out = {}
+        for name, x in xs.items():
+            b = self._pinned(name, x.shape, x.dtype)
+            b.copy_(x, non_blocking=True)
+            out[name] = b
+        self.torch.cuda.current_stream(self.device).synchronize()
+        return {k: v.numpy() for k, v in out.items()}
+
+    def fetch_rows(self, name, x, cap):
+        """x [m, ...] with m <= cap rows into a pinned buffer of cap rows (allocated once): one synchronize."""
+        m = int(x.shape[0])
+        b = self._pinned(name, (cap,) + tuple(x.shape[1:]), x.dtype)
+        if m:
+            b[:m].copy_(x, non_blocking=True)
+            self.torch.cuda.current_stream(self.device).synchronize()
+        return b.numpy()[:m]
+
+    def upload(self, name, host, dev_out):
+        b = self._pinned(name, host.shape, dev_out.dtype)
+        b.numpy()[...] = host
+        dev_out.copy_(b, non_blocking=True)
+        return dev_out
+
+
 class HumanoidVecEnv:
     """Batched LowLevelHumanoidEnv (low_level_env.py:36-526) - one lane per env instance."""
 

@@ -86,3 +86,22 @@ def test_bench_launch_sizes_cover_exactly_the_requested_steps():
             sz = bench.launch_sizes(steps, k)
             assert sum(sz) == steps and all(0 < x <= k for x in sz) and all(x == k for x in sz[:-1])
     assert bench.launch_sizes(0, 32) == []
+
+
+def test_register_envs_vectorised_by_default(monkeypatch):
+    """register_envs() registers the N-lane creators by default (one launch per sampler step for all of a worker's
+    envs): HumanoidBulletEnv-v0-Low -> make_env_low_vec, HumanoidBulletEnv-v0-Hier -> make_env_hier_vec; with
+    vectorised=False the reference's one-env-per-call creators (train_config.py:13-20,320-321)."""
+    reg = {}
+    for name in ("ray", "ray.tune"):
+        monkeypatch.setitem(sys.modules, name, types.ModuleType(name))
+    r = types.ModuleType("ray.tune.registry")
+    r.register_env = lambda name, fn: reg.__setitem__(name, fn)
+    monkeypatch.setitem(sys.modules, "ray.tune.registry", r)
+    import ilrl_amd.hier_env as H
+    import ilrl_amd.low_level_env as L
+    assert L.register_envs() == "HumanoidBulletEnv-v0-Low" and reg["HumanoidBulletEnv-v0-Low"] is L.make_env_low_vec
+    assert H.register_envs() == "HumanoidBulletEnv-v0-Hier" and reg["HumanoidBulletEnv-v0-Hier"] is H.make_env_hier_vec
+    L.register_envs(vectorised=False)
+    H.register_envs(vectorised=False)
+    assert reg["HumanoidBulletEnv-v0-Low"] is L.make_env_low and reg["HumanoidBulletEnv-v0-Hier"] is H.make_env_hier

@@ -19,17 +19,18 @@ extern "C" int dma_copy(void* dst, const void* src, unsigned long long bytes, in
     if (hsa_amd_pointer_info(dst, &pd, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return -3;
     hsa_agent_t da = pd.agentOwner;
     uint32_t mask = 0;
-    if (hsa_amd_memory_copy_engine_status(da, sa, &mask) != HSA_STATUS_SUCCESS) return -4;
+    const hsa_status_t ms = hsa_amd_memory_copy_engine_status(da, sa, &mask);   // may refuse a same-agent pair
     hsa_signal_t sig;
     if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return -5;
-    hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)engine_bit;
-    if (!(mask & (uint32_t)engine_bit)) {   // the requested engine is busy / absent: take the lowest available one
-        for (uint32_t b = 1; b; b <<= 1)
-            if (mask & b) { eng = (hsa_amd_sdma_engine_id_t)b; break; }
+    hsa_status_t st = HSA_STATUS_ERROR;
+    for (uint32_t b = (uint32_t)engine_bit; b && b <= 0x8000u; b <<= 1) {   // the requested engine, else the next ones
+        if (ms == HSA_STATUS_SUCCESS && mask && !(mask & b)) continue;
+        st = hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, bytes, 0, nullptr, sig, (hsa_amd_sdma_engine_id_t)b,
+                                                 true);
+        if (st == HSA_STATUS_SUCCESS) break;
     }
-    hsa_status_t st = hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, bytes, 0, nullptr, sig, eng, true);
     if (st != HSA_STATUS_SUCCESS) { hsa_signal_destroy(sig); return -6; }
     if (wait) hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
     hsa_signal_destroy(sig);
-    return (int)mask;
+    return ms == HSA_STATUS_SUCCESS ? (int)mask : 0;
 }

@@ -50,7 +50,7 @@ def xfer(kind):
         assert r == 0, r
     elif kind == "sdma":
         r = dma.dma_copy(dst.data_ptr(), src.data_ptr(), NB, 1, 1)
-        assert r >= 0, r
+        assert r >= 0, "hsa copy failed: %d" % r
     elif kind == "kernel":
         with torch.cuda.stream(s2):
             dst.view(torch.int32)[: NB // 64].add_(1)
@@ -70,7 +70,7 @@ def timed(fn, reps=5):
 for _ in range(3):
     env_launch()
 res = {"bytes": NB, "env_alone_ms": timed(env_launch)}
-for kind in ("copy_", "peer", "sdma", "kernel"):
+for kind in ("copy_", "peer", "kernel", "sdma"):
     xfer(kind)
     alone = timed(lambda: xfer(kind))
 
@@ -80,6 +80,7 @@ for kind in ("copy_", "peer", "sdma", "kernel"):
     together = timed(both)
     res[kind] = {"alone_ms": alone, "with_env_ms": together,
                  "overlap": (res["env_alone_ms"] + alone - together) / alone}
+    print(kind, json.dumps(res[kind]), flush=True)
     assert torch.equal(dst, src) or kind == "kernel"
     dst.zero_()
 print(json.dumps(res, indent=1))
