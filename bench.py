@@ -58,6 +58,11 @@ def parse():
                     help="initialise torch.distributed and run every collective (barriers, the timing all-reduce, the "
                          "gather) even with one rank: the RCCL code path on a one-GPU box, where RCCL refuses two ranks "
                          "on one device")
+    ap.add_argument("--transport", default="dma", choices=["dma", "collective"],
+                    help="the trajectory gather's transport for N > 1: dma = rank 0 pulls every rank's packed fragment "
+                         "with the SDMA copy engines over IPC-mapped buffers (parallel.DmaGather: no compute unit, so "
+                         "it overlaps the env launches); collective = one dist.gather per fragment (RCCL kernels, which "
+                         "wait for the env launch to leave the CUs)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: host-staged, tests)")
     ap.add_argument("--dump-gather", default=None,
@@ -312,13 +317,14 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     gather_s, gathered, tg = 0.0, [], None
     gdiag = os.environ.get("ILRL_GATHER_DIAG", "")   # diagnostics: "pack" = packing only, "comm" = the gather only
     if G:   # the trajectory gather: static shapes, packed lane-major fragments, asynchronous (parallel.TrajectoryGather)
-        from ilrl_amd.parallel import TrajectoryGather, shard
+        from ilrl_amd.parallel import DmaGather, TrajectoryGather, shard
         o = ring[0] if ring[0] is not None else env.step_k_out(k)
         ring[0] = o
         cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])   # obs (hier: low-level), reward, done
         fields = [("obs", tuple(cols[0].shape[2:]), cols[0].dtype), ("act", (17,), pool[0].dtype),
                   ("reward", tuple(cols[1].shape[2:]), cols[1].dtype), ("done", tuple(cols[2].shape[2:]), cols[2].dtype)]
-        tg = TrajectoryGather(fields, [shard(n * world, world, r)[1] for r in range(world)], G, dev)
+        TG = DmaGather if a.transport == "dma" else TrajectoryGather
+        tg = TG(fields, [shard(n * world, world, r)[1] for r in range(world)], G, dev)
         tg.start(0)   # communicator setup (RCCL point-to-point pairs) outside the timed region
         tg.wait()
     soff[0] = wlaunches
@@ -382,6 +388,8 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / steps   # per env step, on the launch stream (torch's current)
+    if tg is not None and hasattr(tg, "close"):   # outside the timed region: unmap the peers' buffers (collective)
+        tg.close()
     wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if a.dist else wall
     low_steps = None
     if a.hier and a.policy:   # physics env-steps in the timed region: the low-level transitions the rollouts recorded
@@ -612,9 +620,12 @@ def main():
             out["physics_env_steps_per_step"] = phys_steps_per_step
             out["agent_transitions_per_s"] = total / wall_max
         if a.dist and a.gather_every and not a.policy:
-            out["gather"] = {"every": a.gather_every, "backend": a.backend, "to_rank": 0,
-                             "op": "dist.gather of one packed lane-major fragment (RCCL point-to-point), asynchronous, "
-                                   "double-buffered; completed inside the timed region",
+            out["gather"] = {"every": a.gather_every, "backend": a.backend, "to_rank": 0, "transport": a.transport,
+                             "op": ("rank 0 pulls every rank's packed lane-major fragment with the SDMA copy engines "
+                                    "(IPC-mapped buffers, parallel.DmaGather), asynchronous, double-buffered"
+                                    if a.transport == "dma" else
+                                    "dist.gather of one packed lane-major fragment (RCCL point-to-point), "
+                                    "asynchronous, double-buffered") + "; completed inside the timed region",
                              "host_seconds": gather_s, "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1),
                              "fragments": -(-a.steps // a.gather_every)}
         if world == 1 and not a.no_secondary and not a.hier and not a.policy:

@@ -54,7 +54,8 @@ EXPORTS = ["hum_abi_version", "hum_last_error", "hum_default_config", "hum_creat
            "hum_policy_create", "hum_policy_destroy", "hum_policy_act", "hum_rollout", "hum_rollout_fused", "hum_set_terrain",
            "hum_step_k", "hum_hier_step_k", "hum_set_terrain_ex", "hum_policy_act_ex", "hum_policy_create_ex",
            "hum_hier_rollout", "hum_pack_rows", "hum_hier_rollout_fused", "hum_rollout_fused_ex",
-           "hum_hier_rollout_fused_ex"]
+           "hum_hier_rollout_fused_ex", "hum_ipc_export", "hum_ipc_open", "hum_ipc_close", "hum_dma_copy",
+           "hum_dma_wait"]
 
 
 class HumConfig(ctypes.Structure):
@@ -82,6 +83,13 @@ class HumHierTraj(ctypes.Structure):   # hum_hier_traj
 
 
 HUM_PACK_MAX_FIELDS = 6
+
+
+class HumDmaTicket(ctypes.Structure):   # hum_dma_ticket
+    _fields_ = [("signal", ctypes.c_uint64), ("bytes", ctypes.c_uint64)]
+
+
+HUM_IPC_HANDLE_BYTES = 64
 
 
 class HumPackField(ctypes.Structure):   # hum_pack_field
@@ -143,6 +151,11 @@ def lib():
     L.hum_hier_rollout_fused_ex.argtypes = L.hum_hier_rollout.argtypes[:-1] + [vp, vp, vp]
     L.hum_policy_destroy.argtypes = [vp]
     L.hum_pack_rows.argtypes = [ctypes.POINTER(HumPackField), i32, i32, i32, i32, vp]
+    L.hum_ipc_export.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64)]
+    L.hum_ipc_open.argtypes = [ctypes.c_char_p, u64, ctypes.POINTER(vp)]
+    L.hum_ipc_close.argtypes = [vp]
+    L.hum_dma_copy.argtypes = [vp, vp, u64, i32, ctypes.POINTER(HumDmaTicket)]
+    L.hum_dma_wait.argtypes = [ctypes.POINTER(HumDmaTicket)]
     L.hum_policy_act.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, u64, vp]
     L.hum_policy_act_ex.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, i32, u64, vp]
     L.hum_rollout.argtypes = [vp, vp, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]

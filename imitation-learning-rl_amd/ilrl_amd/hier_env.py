@@ -13,6 +13,7 @@
 
 ray is optional (absent in this image): BaseEnv is subclassed only when importable.
 """
+import gc
 import secrets
 
 import numpy as np
@@ -270,34 +271,30 @@ class HierarchicalVectorEnv(_optional_base("ray.rllib.env.base_env", "BaseEnv"))
         runs, and every output comes back in one synchronize (the done lanes' reset rows in a second, only when a
         lane is done); the per-env result dicts are built from whole-array conversions."""
         n = self.num_envs
-        hi_ids, hi_rows, lo_ids, lo_rows = [], [], [], []
-        for i, ad in action_dict.items():
-            if len(ad) != 1:
-                raise AssertionError(ad)
-            for agent_id, act in ad.items():
-                if agent_id == HIGH:
-                    hi_ids.append(i)
-                    hi_rows.append(act)
-                else:
-                    lo_ids.append(i)
-                    lo_rows.append(act)
+        items = action_dict.items()
+        hi = [(i, ad[HIGH]) for i, ad in items if HIGH in ad]
+        lo = [(i, ad[LOW]) for i, ad in items if LOW in ad]
+        if len(hi) + len(lo) != len(action_dict):   # an env with both agents' actions, or neither's
+            raise AssertionError("one action per env and transition (hier_env.py:355-366)")
         agent = np.full(n, N.HUM_AGENT_SEL_SKIP, np.uint8)
-        if hi_ids:
-            self._ah[hi_ids] = np.asarray(hi_rows, dtype=np.float32).reshape(len(hi_ids), 2)
-            agent[hi_ids] = 1
-        if lo_ids:
-            lo = np.asarray(lo_rows, dtype=np.float32).reshape(len(lo_ids), 17)
-            if not np.isfinite(lo).all():
+        if hi:
+            ids, rows = zip(*hi)
+            ids = np.fromiter(ids, np.int64, len(ids))
+            self._ah[ids] = np.concatenate(rows).reshape(len(ids), 2)
+            agent[ids] = 1
+        if lo:
+            ids, rows = zip(*lo)
+            ids = np.fromiter(ids, np.int64, len(ids))
+            la = np.concatenate(rows).reshape(len(ids), 17)
+            if not np.isfinite(la).all():
                 raise AssertionError("non-finite action (humanoid.py:55)")
-            self._al[lo_ids] = lo
-            agent[lo_ids] = 0
+            self._al[ids] = la
+            agent[ids] = 0
         io, d, v = self._io, self._dev, self.venv
         out = v.step(io.upload("ah", self._ah, d["ah"]), io.upload("al", self._al, d["al"]),
                      agent=io.upload("ag", agent, d["ag"]), autoreset=True)
         agents, oh, ol, rh, rl, done, _ = out
         h = io.fetch(agents=agents, oh=oh, ol=ol, rh=rh, rl=rl, done=done)
-        oh64, ol64 = h["oh"].astype(np.float64), h["ol"].astype(np.float64)   # the reference's float64 obs
-        ag, rhl, rll, dn = h["agents"].tolist(), h["rh"].tolist(), h["rl"].tolist(), h["done"].astype(bool).tolist()
         self._reset_rows = {}
         idx = np.flatnonzero(h["done"])
         if idx.size:   # the done lanes' auto-reset high-level observations only (try_reset serves them)
@@ -305,22 +302,29 @@ class HierarchicalVectorEnv(_optional_base("ray.rllib.env.base_env", "BaseEnv"))
                                  n).astype(np.float64)
             self._reset_rows = dict(zip(idx.tolist(), rows))
         self._book_cache = None
+        # the per-env result dicts, from whole-array conversions (the reference's float64 obs); the cyclic garbage
+        # collector is paused while ~5 n acyclic containers are built (it would otherwise rescan them repeatedly)
         AH, AL = N.HUM_AGENT_HIGH, N.HUM_AGENT_LOW
-        obs, rew, dones, infos = {}, {}, {}, {}
-        for i in action_dict:
-            a = ag[i]
-            if a == AH:
-                obs[i], rew[i], infos[i] = {HIGH: oh64[i]}, {HIGH: rhl[i]}, {HIGH: {}}
-            elif a == AL:
-                obs[i], rew[i], infos[i] = {LOW: ol64[i]}, {LOW: rll[i]}, {LOW: {}}
-            else:   # both agents report (the level hand-back, or done)
-                o, r = {}, {}
-                if a & AH:
-                    o[HIGH], r[HIGH] = oh64[i], rhl[i]
-                if a & AL:
-                    o[LOW], r[LOW] = ol64[i], rll[i]
-                obs[i], rew[i], infos[i] = o, r, {k: {} for k in o}
-            dones[i] = {"__all__": dn[i]}
+        acted = list(action_dict)
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            ohr, olr = list(h["oh"].astype(np.float64)), list(h["ol"].astype(np.float64))
+            rhl, rll, agl = h["rh"].tolist(), h["rl"].tolist(), h["agents"].tolist()
+            dnl = h["done"].astype(bool).tolist()
+            if len(acted) != n:
+                agl = [agl[i] for i in acted]
+                dnl = [dnl[i] for i in acted]
+            obs = {i: ({HIGH: ohr[i]} if a == AH else {LOW: olr[i]} if a == AL else
+                       {HIGH: ohr[i], LOW: olr[i]} if a == AH | AL else {}) for i, a in zip(acted, agl)}
+            rew = {i: ({HIGH: rhl[i]} if a == AH else {LOW: rll[i]} if a == AL else
+                       {HIGH: rhl[i], LOW: rll[i]} if a == AH | AL else {}) for i, a in zip(acted, agl)}
+            infos = {i: ({HIGH: {}} if a == AH else {LOW: {}} if a == AL else
+                         {HIGH: {}, LOW: {}} if a == AH | AL else {}) for i, a in zip(acted, agl)}
+            dones = {i: {"__all__": x} for i, x in zip(acted, dnl)}
+        finally:
+            if gc_on:
+                gc.enable()
         self._pending = (obs, rew, dones, infos)
 
     def try_reset(self, env_id):

@@ -15,6 +15,7 @@ gym and ray are optional imports (absent in this image): `LowLevelHumanoidEnv` s
 `HumanoidVectorEnv` subclasses ray.rllib.env.vector_env.VectorEnv when those import; the spaces fall back to
 a minimal Box.
 """
+import gc
 import secrets
 
 import numpy as np
@@ -341,7 +342,13 @@ class HumanoidVectorEnv(_optional_base("ray.rllib.env.vector_env", "VectorEnv"))
                                        self.num_envs).copy()
             self._reset_rows = dict(zip(idx.tolist(), rows))
         self._invalidate()
-        return list(o), h["rew"].tolist(), d.tolist(), [{} for _ in range(self.num_envs)]
+        gc_on = gc.isenabled()   # ~2 n acyclic objects follow: keep the cyclic collector from rescanning them
+        gc.disable()
+        try:
+            return list(o), h["rew"].tolist(), d.tolist(), [{} for _ in range(self.num_envs)]
+        finally:
+            if gc_on:
+                gc.enable()
 
     def get_unwrapped(self):
         return self._views

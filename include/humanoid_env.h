@@ -314,6 +314,27 @@ typedef struct {
 } hum_pack_field;
 int hum_pack_rows(const hum_pack_field* fields, int32_t nfields, int32_t k, int32_t n, int32_t t0, void* stream);
 
+/* ---- The fragment transport without compute units (ABI 14; reference: the rollout workers' sample
+ * batches travel to the learner, train_config.py:33-34).  The env kernel occupies every CU for a launch's whole
+ * duration (a SIMD's register file per wave, a CU's LDS per four blocks), so a collective's kernels cannot run beside
+ * it; the SDMA copy engines can.  Each rank exports its packed send buffers once (hum_ipc_export: a device pointer,
+ * possibly inside a larger allocation, -> handle + offset), the learner rank maps them (hum_ipc_open) and pulls each
+ * fragment with hum_dma_copy (an SDMA engine, forced; over xGMI between GPUs), completing with hum_dma_wait.  Host
+ * calls only: ordering against the streams that produce / consume the buffers is the caller's
+ * (ilrl_amd/parallel.py DmaGather: events and a host control channel). */
+#define HUM_IPC_HANDLE_BYTES 64
+int hum_ipc_export(const void* dev_ptr, uint8_t* handle /* [HUM_IPC_HANDLE_BYTES] */, uint64_t* offset);
+int hum_ipc_open(const uint8_t* handle, uint64_t offset, void** dev_ptr);
+int hum_ipc_close(void* dev_ptr);   /* the pointer hum_ipc_open returned minus its offset (the mapping's base) */
+typedef struct {
+    uint64_t signal;   /* the copy's completion signal (0: none in flight) */
+    uint64_t bytes;
+} hum_dma_ticket;
+/* engine: an index into the SDMA engines the runtime reports for this (dst, src) pair, taken modulo their count, so
+ * concurrent pulls from several peers can spread over engines */
+int hum_dma_copy(void* dst, const void* src, uint64_t bytes, int32_t engine, hum_dma_ticket* ticket);
+int hum_dma_wait(hum_dma_ticket* ticket);
+
 /* ---- On-GPU policy inference: the reference's PPO policy network (train_config.py:107-111,
  * RLlib FullyConnectedNetwork, fcnet_hiddens [256, 256], tanh, free_log_std) evaluated on the env's device
  * buffers, so a sampler loop needs no host round trip.  Weights: host float32, TF kernel layout [in][out]:

@@ -38,10 +38,15 @@ def _port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("ranks,lanes,k,every,steps,stride,backend",
-                         [(2, 2048, 8, 8, 16, 1, "gloo"), (8, 4096, 32, 32, 32, 61, "gloo"), (1, 4096, 32, 32, 64, 7, "nccl")],
-                         ids=["2x2048", "config4_8x4096", "rccl_1x4096"])
-def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride, backend):
+@pytest.mark.parametrize("ranks,lanes,k,every,steps,stride,backend,transport",
+                         [(2, 2048, 8, 8, 16, 1, "gloo", "collective"), (8, 4096, 32, 32, 32, 61, "gloo", "collective"),
+                          (1, 4096, 32, 32, 64, 7, "nccl", "collective"), (2, 2048, 8, 8, 32, 1, "gloo", "dma"),
+                          (8, 4096, 32, 32, 64, 61, "gloo", "dma"), (1, 4096, 32, 32, 64, 7, "nccl", "dma")],
+                         ids=["2x2048", "config4_8x4096", "rccl_1x4096", "dma_2x2048", "dma_config4_8x4096",
+                              "dma_rccl_1x4096"])
+def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride, backend, transport):
+    """transport "dma": the default for N > 1 - IPC-mapped send buffers pulled by rank 0 with the SDMA copy engines
+    (parallel.DmaGather; on one GPU the copies are intra-device, between GPUs they cross xGMI)."""
     import types
     sys.path.insert(0, REPO)
     import bench
@@ -49,7 +54,8 @@ def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, ever
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(ranks),
            "--backend", backend, "--lanes", str(lanes), "--steps", str(steps), "--warmup", "0", "--k", str(k),
-           "--gather-every", str(every), "--dump-gather", dump, "--dump-lane-stride", str(stride), "--cpu-seconds", "0"]
+           "--gather-every", str(every), "--dump-gather", dump, "--dump-lane-stride", str(stride), "--cpu-seconds", "0",
+           "--transport", transport]
     if ranks == 1:   # RCCL refuses two ranks on one device: one rank with every collective run through it
         cmd += ["--force-dist", "--no-secondary"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
@@ -60,7 +66,7 @@ def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, ever
     assert line["n_gpus"] == ranks and line["config"]["steps_per_launch"] == k and line["config"]["launch_sizes"] == [k]
     assert line["config"]["launches"] == steps // k
     assert line["gather"]["every"] == every and line["gather"]["fragments"] == steps // every
-    assert line["gather"]["backend"] == backend
+    assert line["gather"]["backend"] == backend and line["gather"]["transport"] == transport
     assert line["value"] > 0 and line["error_flags"] == 0
     g = np.load(dump)
     total = ranks * lanes

@@ -67,6 +67,34 @@ def timed(fn, reps=5):
     return sorted(ts)[len(ts) // 2] * 1e3
 
 
+def completion_offsets(kind, reps=5):
+    """the transfer issued right AFTER the env launch was enqueued (its waves already own the CUs): when does it
+    complete, measured from the launch's start?  ~alone_ms = it ran beside the launch; ~env_ms = it waited for it."""
+    outs = []
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ex = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        env_launch()
+        e1.record()
+        time.sleep(2e-4)   # the launch's waves are resident before the transfer is issued
+        if kind == "sdma":
+            t0 = time.perf_counter()
+            xfer(kind)   # host-issued, host-waited
+            host_done = (time.perf_counter() - t0) * 1e3 + 0.2
+            torch.cuda.synchronize(dev)
+            outs.append((host_done, e0.elapsed_time(e1)))
+        else:
+            s2.wait_event(e0)
+            xfer(kind)
+            ex.record(s2)
+            torch.cuda.synchronize(dev)
+            outs.append((e0.elapsed_time(ex), e0.elapsed_time(e1)))
+    outs.sort()
+    return outs[len(outs) // 2]
+
+
 for _ in range(3):
     env_launch()
 res = {"bytes": NB, "env_alone_ms": timed(env_launch)}
@@ -80,6 +108,9 @@ for kind in ("copy_", "peer", "kernel", "sdma"):
     together = timed(both)
     res[kind] = {"alone_ms": alone, "with_env_ms": together,
                  "overlap": (res["env_alone_ms"] + alone - together) / alone}
+    done_at, env_ms = completion_offsets(kind)
+    res[kind]["completes_after_launch_start_ms"] = done_at
+    res[kind]["env_launch_ms"] = env_ms
     print(kind, json.dumps(res[kind]), flush=True)
     assert torch.equal(dst, src) or kind == "kernel"
     dst.zero_()
