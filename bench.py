@@ -13,7 +13,7 @@ runs asynchronously beside the next launches and is completed inside the timed r
 
 Prints ONE JSON line on rank 0.  Every number in it is measured in this run except `roofline.traffic`
 (PMC bytes, profiles/pmc_traffic.json, from a rocprofv3 --pmc pass of this same command) and the static FLOP
-count per env-step (profiles/r02_flops_per_env_step.json, tools/flop_count.py).
+count per env-step (profiles/r06_flops_per_env_step.json, tools/flop_count.py).
 """
 import argparse
 import json
@@ -572,7 +572,7 @@ def main():
         total = n * world * a.steps
         phys_steps_per_step = (low_steps / world / a.steps) if a.hier else n   # per GPU, per env step
         value = (low_steps if a.hier else total) / wall_max
-        flops_j = _load_json("profiles/r02_flops_per_env_step.json")
+        flops_j = _load_json("profiles/r06_flops_per_env_step.json")
         flops = flops_j["flops_per_env_step_mean"] if flops_j else None
         achieved = phys_steps_per_step * BYTES_PER_STEP_ALGO / (kern_ms * 1e-3) / 1e9
         traffic = None
@@ -614,7 +614,7 @@ def main():
             tf = phys_steps_per_step * flops / (kern_ms * 1e-3) / 1e12
             out["roofline_valu"] = {"bound": "valu-%s" % a.precision, "achieved": tf, "peak": peak, "unit": "TFLOP/s",
                                     "frac": tf / peak, "flops_per_env_step": flops,
-                                    "source": "profiles/r02_flops_per_env_step.json (tools/flop_count.py)"}
+                                    "source": "profiles/r06_flops_per_env_step.json (tools/flop_count.py)"}
         if a.hier:
             out["unit"] = "env-steps/s"
             out["physics_env_steps_per_step"] = phys_steps_per_step

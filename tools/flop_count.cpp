@@ -47,10 +47,15 @@ static inline F sin(F a) { g_flops++; return F(std::sin(a.v)); }
 static inline F cos(F a) { g_flops++; return F(std::cos(a.v)); }
 static inline F fabs(F a) { return F(std::fabs(a.v)); }
 static inline void sincos(F q, F* s, F* c) { g_flops += 2; *s = F(std::sin(q.v)); *c = F(std::cos(q.v)); }
+// a fused multiply-add: 2 FLOPs unless an operand makes part of it trivial (as for * and +)
+static inline F fma(F a, F b, F c) { return a * b + c; }
+static inline F floor(F a) { return F(std::floor(a.v)); }
 using std::sqrt;
 using std::sin;
 using std::cos;
 using std::fabs;
+using std::fma;
+using std::floor;
 
 #include "../imitation-learning-rl_amd/csrc/physics.h"
 

@@ -2,7 +2,9 @@
 """Summarise rocprofv3 databases (kernel-trace/stats + FETCH_SIZE / WRITE_SIZE passes) into profiles/.
 
 usage: tools/prof_summary.py TAG [prof_root=gpurun_out] [lanes=4096] [clip=motion02_04] [precision=fp32] [k=8]
-(k = env steps per launch of the profiled bench command)
+                             [instantiation=step_group_kernelIfLi4ELb0ELi3E]
+(k = env steps per launch of the profiled bench command; instantiation: the mangled name substring of the profiled
+kernel, whose register / spill counts are read from the shipped code object's metadata note)
 Writes profiles/<TAG>_kernel_stats.txt and updates profiles/pmc_traffic.json (bench.py reads it).
 HBM bytes per launch follow MI355X_MICROARCH.md: FETCH_SIZE counts half the bytes of wide coalesced
 streaming reads on gfx950 (reported both raw and x2); WRITE_SIZE is exact for 16-B stores.
@@ -13,6 +15,29 @@ import sqlite3
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def code_object_meta(kname, inst=None):
+    """The kernel's register / spill / segment sizes from the AMDGPU metadata note of the shipped library's code
+    objects (tools/spill_map.py kernel_meta); the vgpr_count there includes the AGPRs (unified register file).
+    rocprofv3's summary names every instantiation "step_group_kernel": `inst` is the mangled template-argument
+    substring of the one profiled (the benchmarked low-level fp32 kernel, POLICY 3, by default)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from spill_map import kernel_meta
+    from test_cpu_isa import code_objects
+    lib = os.path.join(REPO, "imitation-learning-rl_amd", "ilrl_amd", "_lib", "libhumenv.so")
+    if not os.path.exists(lib):
+        return None
+    tmp = tempfile.mkdtemp()
+    for j, co in enumerate(code_objects(lib)):
+        p = os.path.join(tmp, "co_%d.o" % j)
+        open(p, "wb").write(co)
+        for name, m in kernel_meta(p).items():
+            if (inst or "step_group_kernelIfLi4ELb0ELi3E") in name:
+                return m
+    return None
 
 
 def main():
@@ -37,7 +62,16 @@ def main():
     row = con.execute("select vgpr_count, accum_vgpr_count, sgpr_count, scratch_size, lds_size, workgroup_x, grid_x "
                       "from kernels where name=? limit 1", (kname,)).fetchone()
     if row:
-        out.append("%s resources: vgpr=%s agpr=%s sgpr=%s scratch/lane=%s lds=%s wg=%s grid=%s" % ((kname,) + row))
+        out.append("%s rocprofv3 resources: vgpr=%s agpr=%s sgpr=%s scratch/lane=%s lds=%s wg=%s grid=%s "
+                   "(rocprofv3 reports no AGPRs for this code object: the note below is authoritative)" % ((kname,) + row))
+    meta = code_object_meta(kname, sys.argv[7] if len(sys.argv) > 7 else None)
+    if meta:
+        out.append("%s code object (AMDGPU metadata note of the shipped libhumenv.so): vgpr_count=%s agpr_count=%s "
+                   "vgpr_spill_count=%s sgpr_spill_count=%s private_segment_fixed_size=%s B/lane "
+                   "group_segment_fixed_size=%s B" % (kname, meta.get("vgpr_count"), meta.get("agpr_count", "0"),
+                                                      meta.get("vgpr_spill_count"), meta.get("sgpr_spill_count"),
+                                                      meta.get("private_segment_fixed_size"),
+                                                      meta.get("group_segment_fixed_size")))
     pmc = {}
     for db, ctr in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
         p = os.path.join(root, db, "run_results.db")
