@@ -80,6 +80,10 @@ def parse():
                          "columns RLlib's sampler records - action_dist_inputs, action_logp and vf_preds from a "
                          "value branch of the same shape (random-init) - over the launch's rows")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / parity side measurements")
+    ap.add_argument("--terrain", default="plane", choices=["plane", "random"],
+                    help="ground: the stadium plane (the reference's default scene) or LowLevelHumanoidEnv(useCustomEnv="
+                         "True)'s CustomScene random block terrain, a new one per lane at every reset (humanoid.py:68-144; "
+                         "its own kernel instantiation, heightfield contacts incl. capsule ridges)")
     ap.add_argument("--adapter", action="store_true",
                     help="time the RLlib drop-in path instead of the raw C-ABI launches: HumanoidVectorEnv.vector_step + "
                          "reset_at per done lane (RLlib 1.2 VectorEnv), or with --hier HierarchicalVectorEnv.poll / "
@@ -280,6 +284,9 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         clips = tuple(CLIP_NAMES) if a.clip == "all" else (a.clip,)
         env = HumanoidVecEnv(n, clips=clips, seed=0, device=dev.index, lane_offset=rank * n, precision=precision,
                              block_size=a.block, **phys)
+        if a.terrain == "random":
+            from ilrl_amd import _native as N
+            env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
 
         def step(s, kk=k):
             j = s % len(ring)
@@ -558,6 +565,8 @@ def main():
         raise SystemExit("--k must be >= 1")
     if a.adapter:
         return run_adapter(a, dev, n)
+    if a.terrain != "plane":   # the in-run parity sample and the secondary legs are the plane workload's
+        a.no_secondary = True
     if a.gather_every is None:
         a.gather_every = a.k if world > 1 and not a.policy else 0
     env, wall_max, kern_ms, low_steps, gather_s, gathered, sizes = run(a, world, rank, dev, n, a.precision, a.steps,
@@ -596,7 +605,7 @@ def main():
                                        if a.hier and a.policy else "launch"),
                        "fused": bool(a.policy and a.fused),
                        "sample_batch_columns": bool(a.policy and a.sample_batch),
-                       "envs_per_gpu": n, "clip": a.clip, "k": a.k,
+                       "envs_per_gpu": n, "clip": a.clip, "k": a.k, "terrain": a.terrain,
                        # the launches the timed region actually ran (--steps < k: one shorter launch)
                        "launches": len(sizes), "steps_per_launch": max(sizes),
                        "launch_sizes": sorted(set(sizes), reverse=True),

@@ -409,7 +409,20 @@ def test_sample_batch_columns_match_torch_fp32():
     torch.testing.assert_close(cols["action_dist_inputs"].reshape(-1, 34)[:, :17], mean, atol=2e-5, rtol=0)
     torch.testing.assert_close(cols["action_dist_inputs"].reshape(-1, 34)[:, 17:], torch.log(std).expand(len(obs), 17))
     torch.testing.assert_close(cols["vf_preds"].reshape(-1), vf, atol=2e-5, rtol=0)
-    torch.testing.assert_close(cols["action_logp"].reshape(-1), logp, atol=2e-3, rtol=1e-5)
+    # action_logp: (1) against the same log-density evaluated in float64 from the columns' OWN mean - the fp32
+    # rounding of a 17-term sum of terms up to |t| (17 x 2^-24 x max |t| per row, plus the float32 output); (2) against
+    # torch's from the torch mean, within what the mean's own 2e-5 difference moves it: sum_k |z_k| / std_k x 2e-5
+    lp = cols["action_logp"].reshape(-1).double()
+    a64 = tr["actions"].reshape(-1, 17).double()
+    m64 = cols["action_dist_inputs"].reshape(-1, 34)[:, :17].double()
+    s64 = std.double()
+    terms = -0.5 * ((a64 - m64) / s64) ** 2 - torch.log(s64) - 0.5 * np.log(2 * np.pi)
+    own = terms.sum(-1)
+    tol_own = 17 * 2.0 ** -24 * terms.abs().max(-1).values + 2.0 ** -24 * own.abs() + 1e-6
+    assert ((lp - own).abs() <= tol_own).all(), float(((lp - own).abs() - tol_own).max())
+    dz = ((a64 - mean.double()) / s64 ** 2).abs().sum(-1)   # |d logp / d mean| summed over the 17 dimensions
+    tol_mean = 2e-5 * dz + 17 * 2.0 ** -24 * terms.abs().max(-1).values + tol_own
+    assert ((lp - logp.double()).abs() <= tol_mean).all(), float(((lp - logp.double()).abs() - tol_mean).max())
     env.close()
     pol.close()
     vpol.close()
