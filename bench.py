@@ -330,8 +330,17 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])   # obs (hier: low-level), reward, done
         fields = [("obs", tuple(cols[0].shape[2:]), cols[0].dtype), ("act", (17,), pool[0].dtype),
                   ("reward", tuple(cols[1].shape[2:]), cols[1].dtype), ("done", tuple(cols[2].shape[2:]), cols[2].dtype)]
-        TG = DmaGather if a.transport == "dma" else TrajectoryGather
-        tg = TG(fields, [shard(n * world, world, r)[1] for r in range(world)], G, dev)
+        counts = [shard(n * world, world, r)[1] for r in range(world)]
+        if a.transport == "dma":
+            from ilrl_amd.parallel import DmaUnavailable
+            try:
+                tg = DmaGather(fields, counts, G, dev)
+            except DmaUnavailable as e:   # every rank alike: the collective transport, recorded in the line
+                print("bench: %s; falling back to --transport collective" % e, file=sys.stderr, flush=True)
+                a.transport = "collective (dma unavailable: %s)" % str(e)[:200]
+                tg = TrajectoryGather(fields, counts, G, dev)
+        else:
+            tg = TrajectoryGather(fields, counts, G, dev)
         tg.start(0)   # communicator setup (RCCL point-to-point pairs) outside the timed region
         tg.wait()
     soff[0] = wlaunches
