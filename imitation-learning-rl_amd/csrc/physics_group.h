@@ -2279,14 +2279,28 @@ __device__ __attribute__((always_inline)) void group_substep(const PhysParams& P
             // P of the row being solved, from its reduction one stage earlier (the first row's here)
             T pA = fma(A.meff, A.b - row_sum(A.j0 * n0 + A.j1 * n1), A.lam), pB, pC, pD, dlp = T(0);
             // one stage: X (row k) is solved, Y's (row k+1) reduction runs, W (row k+3) is read; Z is row k+2
+            // (HUM_PGS_STUDY_*: timing-only diagnostic builds for the stall attribution of DESIGN.md section 7 - the
+            // 16-lane DPP reduction replaced by four dependent plain adds, the row-ahead LDS loads by register copies;
+            // their results are meaningless, the trip counts are the real ones)
+#ifdef HUM_PGS_STUDY_NODPP
+            auto rsum = [](T v) { v += v; v += v; v += v; v += v; return v; };
+#else
+            auto rsum = [](T v) { return row_sum(v); };
+#endif
             auto stage = [&](auto masked, int kk, const RowRegs& X, const RowRegs& Y, RowRegs& W, const RowRegs& Z, int oX,
                              int& oW, T pX, T& pY, T lnX, T& lnW) {
                 oW = X.next3;
+#ifdef HUM_PGS_STUDY_NOLOAD
+                W = Z;
+                W.next3 = X.next3;
+                lnW = lnX;
+#else
                 load(oW, W);
                 lnW = load_ln(X.next3_ln);
+#endif
                 // the row-ahead loads issue at the top of their stage: ALU work may cross this point, LDS ops may not
                 __builtin_amdgcn_sched_barrier(0x407);
-                pY = fma(Y.meff, Y.b - row_sum(Y.j0 * n0 + Y.j1 * n1), Y.lam);
+                pY = fma(Y.meff, Y.b - rsum(Y.j0 * n0 + Y.j1 * n1), Y.lam);
                 const T lo = -(X.mu * lnX), hi = X.hi + X.mu * lnX;
                 const T tX = fma(-X.q, dlp, pX);
                 const T lsol = med3(tX, lo, hi);   // == clamp: lo <= hi always
