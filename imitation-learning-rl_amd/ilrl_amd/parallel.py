@@ -9,6 +9,7 @@
 """
 import ctypes
 import math
+import os
 import queue
 import threading
 
@@ -247,6 +248,8 @@ class DmaGather(TrajectoryGather):
                         p = ctypes.c_void_p()
                         N.check(L.hum_ipc_open(hb, off, ctypes.byref(p)), "hum_ipc_open")
                         self.remote[r].append((p.value, p.value - off))
+                if os.environ.get("ILRL_AMD_DMA_PROBE_FAIL") == "1":   # tests: the fallback path
+                    raise RuntimeError("injected probe failure (ILRL_AMD_DMA_PROBE_FAIL)")
                 # probe: one small pull from every mapped slot (and the own one) on the copy engines
                 for r in range(self.world):
                     for j in range(slots):
@@ -293,43 +296,57 @@ class DmaGather(TrajectoryGather):
             self._wait_free(j)
 
     def _helper(self):
+        """The transfer loop (one fragment per job).  A failure on any rank is passed on as a negative message, so
+        every rank's helper stops and its main thread raises from pack / wait instead of waiting forever."""
         L = self.N.lib()
         msg = torch.zeros(1, dtype=torch.int64)
+        send = lambda v, r: dist.send(torch.tensor([v], dtype=torch.int64), r, group=self.ctrl)
         try:
             while True:
                 job = self.jobs.get()
                 if job is None:
                     return
                 f, slot, ev = job
-                ev.synchronize()
                 if self.rank != self.dst:
-                    dist.send(torch.tensor([f], dtype=torch.int64), self.dst, group=self.ctrl)   # packed
-                    dist.recv(msg, self.dst, group=self.ctrl)                                      # pulled
+                    try:
+                        ev.synchronize()
+                    except Exception:
+                        send(-1, self.dst)
+                        raise
+                    send(f, self.dst)                           # packed
+                    dist.recv(msg, self.dst, group=self.ctrl)   # pulled
                     if int(msg.item()) != f:
-                        raise RuntimeError("fragment %d acknowledged as %d" % (f, int(msg.item())))
+                        raise RuntimeError("fragment %d: the learner answered %d" % (f, int(msg.item())))
                 else:
-                    tickets, eng = [], 0
-                    for r in range(self.world):
-                        rows = self.counts[r]
-                        dst_ptr = self.recv[slot][r].data_ptr()
-                        if r == self.dst:   # its own fragment: also a copy-engine transfer
-                            src_ptr = self.send[slot].data_ptr()
-                        else:
-                            dist.recv(msg, r, group=self.ctrl)
-                            if int(msg.item()) != f:
-                                raise RuntimeError("rank %d sent fragment %d, expected %d" % (r, int(msg.item()), f))
-                            src_ptr = self.remote[r][slot][0]
-                        if rows:
-                            t = self.N.HumDmaTicket()
-                            self.N.check(L.hum_dma_copy(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr),
-                                                        rows * self.W, eng, ctypes.byref(t)), "hum_dma_copy")
-                            tickets.append(t)
-                            eng += 1
-                    for t in tickets:
-                        self.N.check(L.hum_dma_wait(ctypes.byref(t)), "hum_dma_wait")
+                    tickets = []
+                    try:
+                        ev.synchronize()
+                        for r in range(self.world):
+                            if r == self.dst:   # its own fragment: also a copy-engine transfer
+                                src_ptr = self.send[slot].data_ptr()
+                            else:
+                                dist.recv(msg, r, group=self.ctrl)
+                                if int(msg.item()) != f:
+                                    raise RuntimeError("rank %d sent %d for fragment %d" % (r, int(msg.item()), f))
+                                src_ptr = self.remote[r][slot][0]
+                            if self.counts[r]:
+                                t = self.N.HumDmaTicket()
+                                self.N.check(L.hum_dma_copy(ctypes.c_void_p(self.recv[slot][r].data_ptr()),
+                                                            ctypes.c_void_p(src_ptr), self.counts[r] * self.W,
+                                                            len(tickets), ctypes.byref(t)), "hum_dma_copy")
+                                tickets.append(t)
+                        while tickets:
+                            self.N.check(L.hum_dma_wait(ctypes.byref(tickets.pop(0))), "hum_dma_wait")
+                    except Exception:
+                        for t in tickets:   # retire the copies in flight before giving up
+                            L.hum_dma_wait(ctypes.byref(t))
+                        for r in range(self.world):
+                            if r != self.dst:
+                                send(-1, r)
+                        raise
                     for r in range(self.world):
                         if r != self.dst:
-                            dist.send(torch.tensor([f], dtype=torch.int64), r, group=self.ctrl)
+                            send(f, r)                          # pulled
                 self.free[slot].set()
         except Exception as e:   # surfaced on the main thread by pack / wait
             self.err.append(repr(e))

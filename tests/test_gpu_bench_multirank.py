@@ -41,9 +41,10 @@ def _port():
 @pytest.mark.parametrize("ranks,lanes,k,every,steps,stride,backend,transport",
                          [(2, 2048, 8, 8, 16, 1, "gloo", "collective"), (8, 4096, 32, 32, 32, 61, "gloo", "collective"),
                           (1, 4096, 32, 32, 64, 7, "nccl", "collective"), (2, 2048, 8, 8, 32, 1, "gloo", "dma"),
-                          (8, 4096, 32, 32, 64, 61, "gloo", "dma"), (1, 4096, 32, 32, 64, 7, "nccl", "dma")],
+                          (8, 4096, 32, 32, 64, 61, "gloo", "dma"), (1, 4096, 32, 32, 64, 7, "nccl", "dma"),
+                          (2, 2048, 8, 8, 16, 1, "gloo", "dma_fallback")],
                          ids=["2x2048", "config4_8x4096", "rccl_1x4096", "dma_2x2048", "dma_config4_8x4096",
-                              "dma_rccl_1x4096"])
+                              "dma_rccl_1x4096", "dma_fallback_2x2048"])
 def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride, backend, transport):
     """transport "dma": the default for N > 1 - IPC-mapped send buffers pulled by rank 0 with the SDMA copy engines
     (parallel.DmaGather; on one GPU the copies are intra-device, between GPUs they cross xGMI)."""
@@ -59,6 +60,9 @@ def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, ever
     if ranks == 1:   # RCCL refuses two ranks on one device: one rank with every collective run through it
         cmd += ["--force-dist", "--no-secondary"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    if transport == "dma_fallback":   # the copy engines refused on one rank: every rank takes the collective path
+        env["ILRL_AMD_DMA_PROBE_FAIL"] = "1"
+        cmd[cmd.index("--transport") + 1] = "dma"
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=560, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
@@ -66,7 +70,10 @@ def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, ever
     assert line["n_gpus"] == ranks and line["config"]["steps_per_launch"] == k and line["config"]["launch_sizes"] == [k]
     assert line["config"]["launches"] == steps // k
     assert line["gather"]["every"] == every and line["gather"]["fragments"] == steps // every
-    assert line["gather"]["backend"] == backend and line["gather"]["transport"] == transport
+    if transport == "dma_fallback":
+        assert line["gather"]["transport"].startswith("collective (dma unavailable"), line["gather"]["transport"]
+    else:
+        assert line["gather"]["backend"] == backend and line["gather"]["transport"] == transport
     assert line["value"] > 0 and line["error_flags"] == 0
     g = np.load(dump)
     total = ranks * lanes
