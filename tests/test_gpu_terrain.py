@@ -302,3 +302,42 @@ def _ridge_fp32_gate(env, terrain, a, clip, lane_quantiles=((50, 1.0), (90, 1.5)
     # absolutely: these pressed-in poses are stiffer than the reset poses FP32_TERRAIN_BOUND was set on (the fp32
     # oracle itself moves their obs by up to ~5e-3), so the bound is the yardstick's own largest envelope, doubled
     assert kern[good].max() <= max(FP32_TERRAIN_BOUND["obs_max"], 2 * envl[good].max()), kern[good].max()
+
+
+def test_random_terrain_rollout_at_scale_fp64():
+    """1024 lanes over CustomScene's random blocks, 60 random-action steps with auto-reset (a new terrain per reset),
+    then one fp64 step of 128 sampled lanes from their injected state vs the oracle: the states the rollout reaches
+    include limbs across block edges (ridge contacts counted from the oracle), and every sampled lane matches (state
+    1e-6, obs / reward 1e-5, done / frame / RNG counter exact; the fp64 tolerances of tests/test_gpu_scale.py)."""
+    n = 1024
+    clip = load_clip(CLIP)
+    terrain = O.Terrain(O.TERRAIN_RANDOM_BLOCKS)
+    env = HumanoidVecEnv(n, clips=(CLIP,), seed=31, precision="fp64")
+    env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
+    env.reset()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(60):
+        env.step(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
+    assert env.error_flags() & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
+    phys, book = env.get_state()
+    a = np.random.default_rng(9).uniform(-1, 1, (n, 17)).astype(np.float32)
+    obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
+    phys2, book2 = env.get_state()
+    env.close()
+    ridge_lanes = 0
+    worst = {"state": 0.0, "obs": 0.0, "rew": 0.0}
+    for i in np.linspace(0, n - 1, 128).astype(int):
+        key = int(book[i, BK["terrain_key_lo"]]) | (int(book[i, BK["terrain_key_hi"]]) << 32)
+        P = terrain.apply(O.default_params(), key)
+        segs = O.geom_segments(phys[i])
+        ridge_lanes += any(O.ridge_contacts(segs[gg, :3], segs[gg, 3:6], segs[gg, 6], P) for gg in range(17)
+                           if segs[gg, 7])
+        o = oracle_from_lane(clip, phys[i], book[i])
+        o.terrain = terrain
+        ro, rr, rd, _ = o.step(a[i])
+        worst["state"] = max(worst["state"], float(np.abs(phys2[i] - o.state).max()))
+        worst["obs"] = max(worst["obs"], float(np.abs(obs[i] - ro).max()))
+        worst["rew"] = max(worst["rew"], abs(float(rew[i]) - rr))
+        assert bool(done[i]) == rd and int(frame[i]) == o.frame and int(book2[i, BK["rng_counter"]]) == o.rng.counter
+    print("terrain rollout fp64: %d of 128 sampled lanes with ridge contacts; worst %s" % (ridge_lanes, worst))
+    assert worst["state"] < 1e-6 and worst["obs"] < 1e-5 and worst["rew"] < 1e-5
