@@ -305,8 +305,8 @@ def _ridge_fp32_gate(env, terrain, a, clip, lane_quantiles=((50, 1.0), (90, 1.5)
 
 
 def test_random_terrain_rollout_at_scale_fp64():
-    """1024 lanes over CustomScene's random blocks, 60 random-action steps with auto-reset (a new terrain per reset),
-    then one fp64 step of 128 sampled lanes from their injected state vs the oracle: the states the rollout reaches
+    """1024 lanes over CustomScene's random blocks, placed anywhere within 20 m, 20 random-action steps with auto-reset
+    (a new terrain per reset), then one fp64 step of 128 sampled lanes from their injected state vs the oracle: the states the rollout reaches
     include limbs across block edges (ridge contacts counted from the oracle), and every sampled lane matches (state
     1e-6, obs / reward 1e-5, done / frame / RNG counter exact; the fp64 tolerances of tests/test_gpu_scale.py)."""
     n = 1024
@@ -315,8 +315,9 @@ def test_random_terrain_rollout_at_scale_fp64():
     env = HumanoidVecEnv(n, clips=(CLIP,), seed=31, precision="fp64")
     env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
     env.reset()
+    _place(env, terrain, np.random.default_rng(13), (-20, 20, -20, 20))   # off the flat centre blocks
     g = torch.Generator(device="cuda").manual_seed(5)
-    for _ in range(60):
+    for _ in range(20):   # falling onto the blocks (a reset lane starts again at the flat centre)
         env.step(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
     assert env.error_flags() & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
     phys, book = env.get_state()
@@ -340,4 +341,5 @@ def test_random_terrain_rollout_at_scale_fp64():
         worst["rew"] = max(worst["rew"], abs(float(rew[i]) - rr))
         assert bool(done[i]) == rd and int(frame[i]) == o.frame and int(book2[i, BK["rng_counter"]]) == o.rng.counter
     print("terrain rollout fp64: %d of 128 sampled lanes with ridge contacts; worst %s" % (ridge_lanes, worst))
+    assert ridge_lanes > 0, "no sampled lane had a limb across a block edge"
     assert worst["state"] < 1e-6 and worst["obs"] < 1e-5 and worst["rew"] < 1e-5
