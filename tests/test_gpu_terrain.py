@@ -305,9 +305,9 @@ def _ridge_fp32_gate(env, terrain, a, clip, lane_quantiles=((50, 1.0), (90, 1.5)
 
 
 def test_random_terrain_rollout_at_scale_fp64():
-    """1024 lanes over CustomScene's random blocks, placed anywhere within 20 m, 20 random-action steps with auto-reset
-    (a new terrain per reset), then one fp64 step of 128 sampled lanes from their injected state vs the oracle: the states the rollout reaches
-    include limbs across block edges (ridge contacts counted from the oracle), and every sampled lane matches (state
+    """1024 lanes over CustomScene's random blocks, placed anywhere within 20 m, 12 random-action steps with auto-reset
+    (a new terrain per reset), then one fp64 step from the injected state vs the oracle for every lane whose limbs lie
+    across a block edge (ridge contacts, found by the oracle) and 64 more: every compared lane matches (state
     1e-6, obs / reward 1e-5, done / frame / RNG counter exact; the fp64 tolerances of tests/test_gpu_scale.py)."""
     n = 1024
     clip = load_clip(CLIP)
@@ -317,7 +317,7 @@ def test_random_terrain_rollout_at_scale_fp64():
     env.reset()
     _place(env, terrain, np.random.default_rng(13), (-20, 20, -20, 20))   # off the flat centre blocks
     g = torch.Generator(device="cuda").manual_seed(5)
-    for _ in range(20):   # falling onto the blocks (a reset lane starts again at the flat centre)
+    for _ in range(12):   # falling onto the blocks (a reset lane starts again at the flat centre)
         env.step(torch.rand(n, 17, device="cuda", generator=g) * 2 - 1, autoreset=True)
     assert env.error_flags() & (N.HUM_EFLAG_CONTACT_OVERFLOW | N.HUM_EFLAG_NONFINITE_ACTION) == 0
     phys, book = env.get_state()
@@ -325,14 +325,16 @@ def test_random_terrain_rollout_at_scale_fp64():
     obs, rew, done, frame = [x.cpu().numpy() for x in env.step(torch.as_tensor(a, device="cuda"))]
     phys2, book2 = env.get_state()
     env.close()
-    ridge_lanes = 0
-    worst = {"state": 0.0, "obs": 0.0, "rew": 0.0}
-    for i in np.linspace(0, n - 1, 128).astype(int):
+    def has_ridge(i):
         key = int(book[i, BK["terrain_key_lo"]]) | (int(book[i, BK["terrain_key_hi"]]) << 32)
         P = terrain.apply(O.default_params(), key)
         segs = O.geom_segments(phys[i])
-        ridge_lanes += any(O.ridge_contacts(segs[gg, :3], segs[gg, 3:6], segs[gg, 6], P) for gg in range(17)
-                           if segs[gg, 7])
+        return any(O.ridge_contacts(segs[gg, :3], segs[gg, 3:6], segs[gg, 6], P) for gg in range(17) if segs[gg, 7])
+    ridge = [i for i in range(n) if has_ridge(i)]   # every lane with a limb across a block edge, + a spread sample
+    sample = sorted(set(ridge) | set(np.linspace(0, n - 1, 64).astype(int).tolist()))
+    ridge_lanes = len(ridge)
+    worst = {"state": 0.0, "obs": 0.0, "rew": 0.0}
+    for i in sample:
         o = oracle_from_lane(clip, phys[i], book[i])
         o.terrain = terrain
         ro, rr, rd, _ = o.step(a[i])
@@ -340,6 +342,7 @@ def test_random_terrain_rollout_at_scale_fp64():
         worst["obs"] = max(worst["obs"], float(np.abs(obs[i] - ro).max()))
         worst["rew"] = max(worst["rew"], abs(float(rew[i]) - rr))
         assert bool(done[i]) == rd and int(frame[i]) == o.frame and int(book2[i, BK["rng_counter"]]) == o.rng.counter
-    print("terrain rollout fp64: %d of 128 sampled lanes with ridge contacts; worst %s" % (ridge_lanes, worst))
-    assert ridge_lanes > 0, "no sampled lane had a limb across a block edge"
+    print("terrain rollout fp64: %d of %d lanes with ridge contacts, %d lanes compared; worst %s" % (
+        ridge_lanes, n, len(sample), worst))
+    assert ridge_lanes > 0, "no lane had a limb across a block edge"
     assert worst["state"] < 1e-6 and worst["obs"] < 1e-5 and worst["rew"] < 1e-5
