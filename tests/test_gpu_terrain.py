@@ -315,6 +315,7 @@ def test_random_terrain_rollout_at_scale_fp64():
     env = HumanoidVecEnv(n, clips=(CLIP,), seed=31, precision="fp64")
     env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
     env.reset()
+    env.set_modes(debug=True)   # step(action, debug=True): done on a fall only (the walk target stays near the origin)
     _place(env, terrain, np.random.default_rng(13), (-20, 20, -20, 20))   # off the flat centre blocks
     g = torch.Generator(device="cuda").manual_seed(5)
     for _ in range(12):   # falling onto the blocks (a reset lane starts again at the flat centre)
