@@ -338,7 +338,7 @@ def test_random_terrain_rollout_at_scale_fp64():
     for i in sample:
         o = oracle_from_lane(clip, phys[i], book[i])
         o.terrain = terrain
-        ro, rr, rd, _ = o.step(a[i])
+        ro, rr, rd, _ = o.step(a[i], debug=True)
         worst["state"] = max(worst["state"], float(np.abs(phys2[i] - o.state).max()))
         worst["obs"] = max(worst["obs"], float(np.abs(obs[i] - ro).max()))
         worst["rew"] = max(worst["rew"], abs(float(rew[i]) - rr))
