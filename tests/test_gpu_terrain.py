@@ -308,7 +308,9 @@ def test_random_terrain_rollout_at_scale_fp64():
     """1024 lanes over CustomScene's random blocks, placed anywhere within 20 m, 12 random-action steps with auto-reset
     (a new terrain per reset), then one fp64 step from the injected state vs the oracle for every lane whose limbs lie
     across a block edge (ridge contacts, found by the oracle) and 64 more: every compared lane matches (state
-    1e-6, obs / reward 1e-5, done / frame / RNG counter exact; the fp64 tolerances of tests/test_gpu_scale.py)."""
+    1e-6, obs / reward 1e-5, done / frame / RNG counter exact; the fp64 tolerances of tests/test_gpu_scale.py).
+    Limbs across an edge are rare in rollouts (1 lane of 1024 here: a humanoid lying on the blocks has fallen, which
+    ends the episode); test_limbs_across_block_edges_match_oracle covers 64 such poses directly."""
     n = 1024
     clip = load_clip(CLIP)
     terrain = O.Terrain(O.TERRAIN_RANDOM_BLOCKS)
