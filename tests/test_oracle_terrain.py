@@ -251,3 +251,43 @@ def test_random_blocks_limbs_across_block_edges():
         seen += len(rl)
     print("ridge contacts", seen)
     assert seen >= 10, seen
+
+
+def test_ridge_contact_invariants_random_capsules():
+    """Every ridge contact of random capsules over CustomScene's blocks satisfies the model's invariants: a unit
+    normal, its axis point clear of both end caps (t L > 0.02 and (1 - t) L > 0.02), the terrain point on the surface
+    at signed distance d from the capsule (|s - pb| = r + d along n; when the axis point is inside the terrain, the
+    face-normal branch's projection onto the plane under it), d below the contact threshold, at most two per capsule
+    and none within 0.02 m of another along the axis."""
+    terrain = O.Terrain(O.TERRAIN_RANDOM_BLOCKS)
+    key = O.next_terrain_key(0, O.lane_key(3, 9))
+    P = terrain.apply(O.default_params(), key)
+    rng = np.random.default_rng(21)
+    found = 0
+    for _ in range(4000):
+        c = rng.uniform([-30, -30, 0.0], [30, 30, 0.0])
+        c[2] = _surface_height(terrain, key, c[0], c[1]) + rng.uniform(0.0, 0.12)
+        half = rng.uniform(0.05, 0.25)
+        d = rng.normal(size=3)
+        d[2] *= 0.2   # mostly lying
+        d /= np.linalg.norm(d)
+        a, b, r = c - half * d, c + half * d, rng.uniform(0.03, 0.06)
+        rc = O.ridge_contacts(a, b, r, P)
+        assert len(rc) <= 2
+        L = 2 * half
+        ts = []
+        for n, dist, t in rc:
+            found += 1
+            assert abs(np.linalg.norm(n) - 1) < 1e-12
+            assert t * L > 0.02 - 1e-12 and (1 - t) * L > 0.02 - 1e-12
+            assert dist < P.contact_thresh
+            s = a + t * (b - a)
+            pb = s - (r + dist) * n
+            if s[2] > _surface_height(terrain, key, s[0], s[1]):   # the closest-point branch: pb on the surface
+                assert abs(pb[2] - _surface_height(terrain, key, pb[0], pb[1])) < 1e-9
+            else:   # axis point inside the terrain: the face-normal branch projects onto the plane under s
+                assert abs(pb[2] - _surface_height(terrain, key, pb[0], pb[1])) < 1e-3
+            ts.append(t)
+        if len(ts) == 2:
+            assert abs(ts[0] - ts[1]) * L >= 0.02
+    assert found >= 20, found
