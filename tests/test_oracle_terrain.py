@@ -167,11 +167,24 @@ def test_capsule_across_a_ridge_tilted_and_valley():
     b = np.array([0.9, 0.3, _surface_z(t, 0.5) + r + 0.005 + 0.4 * 0.02])
     rc = O.ridge_contacts(a, b, r, P)
     assert len(rc) == 1 and 0.4 < rc[0][2] < 0.6
-    # a valley (concave edge): no ridge contact anywhere along the axis; the end caps carry the contacts
+    # a valley (concave edge): no ridge contact anywhere along the axis; the end caps carry the contacts, one on
+    # each facet with that facet's normal (-/+0.2, 0, 1)/|.| and the closed-form distance
     v = _roof(sign=-1.0)
     Pv = v.apply(O.default_params())
-    zv = (0.3 + 0.2 * 0.7) - v.mid
-    assert O.ridge_contacts(np.array([-0.2, 0.3, zv]), np.array([1.2, 0.3, zv]), r, Pv) == []
+    zv = float(np.float32(0.3 + 0.2 * 0.7)) - v.mid
+    a, b = np.array([-0.2, 0.3, zv]), np.array([1.2, 0.3, zv])
+    assert O.ridge_contacts(a, b, r, Pv) == []
+    f = O.lib().om_terrain_contact
+    dp = ctypes.POINTER(ctypes.c_double)
+    f.argtypes = [ctypes.POINTER(O.OmParams), dp, ctypes.c_double, dp, dp]
+    for end, sx in ((a, -1.0), (b, 1.0)):
+        n, d = np.zeros(3), np.zeros(1)
+        assert f(ctypes.byref(Pv), O._p(end), r, O._p(n), O._p(d)) == 1
+        want = np.array([sx * -0.2, 0.0, 1.0]) / np.sqrt(1.04)
+        np.testing.assert_allclose(n, want, atol=1e-6)
+        # the end sits on its facet's surface height: distance to the facet plane = height gap x cos(slope) - r
+        zs = float(np.float32(0.3 + 0.2 * abs(end[0] - 0.5))) - v.mid
+        np.testing.assert_allclose(d[0], (end[2] - zs) / np.sqrt(1.04) - r, atol=1e-6)
     # parallel to the ridge (never crossing an edge's interior transversally): the ridge line itself is the minimum
     # all along, so the closest points fall at an axis end - the end caps' contacts, no ridge contact
     zr = _surface_z(t, 0.5) + r + 0.005
