@@ -219,13 +219,28 @@ def launch_sizes(steps, k):
     return [k] * (steps // k) + ([steps % k] if steps % k else [])
 
 
+def launch_plan(steps, k, drain=False):
+    """The timed launches as (action block, first row in it, env steps): launch_sizes' launches, block b of the
+    device-resident action pool for launch b.  drain (the chunked copy-engine gather): the last launch's final fifth
+    is split off into its own launch - same action rows, same trajectory bit for bit - so that what the gather still
+    moves after the last launch ends is that short launch's rows, while the rest of the last launch's rows travel
+    during it (a chunk's pull takes ~a fifth of the launch time that produced it)."""
+    plan = [(b, 0, kk) for b, kk in enumerate(launch_sizes(steps, k))]
+    if drain and plan and plan[-1][2] >= 2:
+        b, _, kk = plan.pop()
+        d = max(1, round(kk / 5))
+        plan += [(b, 0, kk - d), (b, kk - d, d)]
+    return plan
+
+
 def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     """Build the env, warm up, time `steps` env steps in launches of k.  Returns (env, wall_max_s, kernel_ms per
     env step, low_steps, gather_s, gathered, the timed launches' sizes)."""
     import torch
     import torch.distributed as dist
     k = k or a.k
-    sizes, wsizes = launch_sizes(steps, k), launch_sizes(warmup, k)
+    plan, wsizes = launch_plan(steps, k), launch_sizes(warmup, k)
+    sizes = [p[2] for p in plan]
     launches, wlaunches = len(sizes), len(wsizes)
     pool, hpool = _pools(a, dev, n, k, rank)
     G = a.gather_every if a.dist and not a.policy else 0
@@ -239,10 +254,11 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         env = HierVecEnv(n, seed=0, device=dev.index, lane_offset=rank * n, precision=precision, block_size=a.block,
                          **phys)
 
-        def step(s, kk=k):
+        def step(s, kk=k, o=0):
             j = s % len(ring)
-            if kk < k:   # the remainder launch
-                return env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True, out=rem_out.get(kk))
+            if kk < k:   # the remainder launch (or the drain launches: rows o .. o + kk of block s)
+                return env.step_k(hpool[s % 16][o:o + kk], pool[s % 16][o:o + kk], autoreset=True,
+                                  out=rem_out.get(kk))
             ring[j] = env.step_k(hpool[s % 16], pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:   # config 5 closed loop: both levels' policies on the device (hum_hier_rollout[_fused])
             from ilrl_amd.policy import DevicePolicy, hier_rollout, hier_traj_buffers
@@ -264,7 +280,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
                 vlow = DevicePolicy.random_init_value(seed=37 + rank, device=dev.index)
             cols_out = {}
 
-            def step(s, kk=k):   # launch numbers (and the exploration noise's step index) continue past the warm-up
+            def step(s, kk=k, o=0):   # launch numbers (and the exploration noise's step index) continue past the warm-up
                 tr = hier_rollout(env, high, low, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True,
                                   fused=a.fused, out=traj_bufs(kk, s), means=mtr)
                 if a.sample_batch:   # both agents' columns; rows of the agent that did not act are zeroed
@@ -288,17 +304,17 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             from ilrl_amd import _native as N
             env.set_terrain(N.HUM_TERRAIN_RANDOM_BLOCKS)
 
-        def step(s, kk=k):
+        def step(s, kk=k, o=0):
             j = s % len(ring)
-            if kk < k:   # the remainder launch
-                return env.step_k(pool[s % 16][:kk], autoreset=True, out=rem_out.get(kk))
+            if kk < k:   # the remainder launch (or the drain launches: rows o .. o + kk of block s)
+                return env.step_k(pool[s % 16][o:o + kk], autoreset=True, out=rem_out.get(kk))
             ring[j] = env.step_k(pool[s % 16], autoreset=True, out=ring[j])
         if a.policy:
             from ilrl_amd.policy import DevicePolicy
             pol = DevicePolicy.random_init(seed=7 + rank, device=dev.index)
             actbuf = torch.zeros(n, 17, device=dev)
 
-            def step(s, kk=1):
+            def step(s, kk=1, o=0):
                 pol.act(env.obs, env.obs_reset, env.done, explore=True, step=s + soff[0], out=actbuf)
                 return env.step(actbuf, autoreset=True)
             if a.fused:   # the policy inside the multi-step env kernel (hum_rollout_fused), trajectories recorded
@@ -307,7 +323,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
                 vpol = DevicePolicy.random_init_value(seed=27 + rank, device=dev.index) if a.sample_batch else None
                 cols_out = {}
 
-                def step(s, kk=k):
+                def step(s, kk=k, _o=0):
                     o = traj_out.get(kk)
                     tr = pol.rollout(env, kk, explore=True, step0=(s + soff[0]) * k, trajectories=True, fused=True,
                                      out=o, means=a.sample_batch)
@@ -323,7 +339,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         step(w, wsizes[w])
     gather_s, gathered, tg = 0.0, [], None
     gdiag = os.environ.get("ILRL_GATHER_DIAG", "")   # diagnostics: "pack" = packing only, "comm" = the gather only
-    if G:   # the trajectory gather: static shapes, packed lane-major fragments, asynchronous (parallel.TrajectoryGather)
+    if G:   # the trajectory gather: static shapes, packed step-major fragments, asynchronous (parallel.TrajectoryGather)
         from ilrl_amd.parallel import DmaGather, TrajectoryGather, shard
         o = ring[0] if ring[0] is not None else env.step_k_out(k)
         ring[0] = o
@@ -343,6 +359,10 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
             tg = TrajectoryGather(fields, counts, G, dev)
         tg.start(0)   # communicator setup (RCCL point-to-point pairs) outside the timed region
         tg.wait()
+        if isinstance(tg, DmaGather):   # per-launch chunks: end on a short drain launch
+            plan = launch_plan(steps, k, drain=True)
+            sizes, launches = [p[2] for p in plan], len(plan)
+            a.drain = plan[-1][2] if len(plan) > len(launch_sizes(steps, k)) else None
     soff[0] = wlaunches
     if a.hier and a.policy:   # the timed launches' trajectory buffers
         for s, kk in enumerate(sizes):
@@ -373,28 +393,27 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for s in range(launches):
-        step(s, sizes[s])
+    done_steps = 0
+    for s, (b, ro, kk) in enumerate(plan):
+        step(b, kk, ro)
         if tg is not None:
             th = time.perf_counter()
-            slot = (s * k // G) % 2
-            o = ring[0]
+            slot, f0 = (done_steps // G) % 2, done_steps % G   # the fragment slot, the launch's first step in it
+            o = ring[0] if kk == k else rem_out[kk]   # the launch's outputs (full, remainder or drain launch)
             cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])
-            kk = sizes[s]
-            act = pool[s % 16][:kk]
-            if kk < k:   # the remainder launch's outputs
-                o = rem_out[kk]
-                cols = (o[2], o[4], o[5]) if a.hier else (o[0], o[1], o[2])
+            act = pool[b % 16][ro:ro + kk]
+            final = (done_steps + kk) % G == 0 or s == launches - 1   # a full fragment, or the last one
             if gdiag != "comm":
-                tg.pack(slot, (s * k) % G, {"obs": cols[0], "act": act, "reward": cols[1], "done": cols[2]})
-            if gdiag != "pack" and ((s * k + kk) % G == 0 or s == launches - 1):   # a full fragment, or the last one
-                tg.start(slot)
-                if a.dump_gather:   # tests: rank 0 keeps the fragment (synchronous)
+                tg.pack(slot, f0, {"obs": cols[0], "act": act, "reward": cols[1], "done": cols[2]})
+            if gdiag != "pack":
+                tg.commit(slot, f0, f0 + kk, final)
+                if final and a.dump_gather:   # tests: rank 0 keeps the fragment (synchronous)
                     tg.wait(slot)
                     got = tg.result(slot)
                     if got is not None:
                         gathered.append([got[f][::a.dump_lane_stride].cpu() for f in ("obs", "act", "reward", "done")])
             gather_s += time.perf_counter() - th
+        done_steps += kk
     if tg is not None:
         tg.wait()   # the last fragments' gathers complete inside the timed region
     ev1.record(stream)
@@ -404,6 +423,9 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / steps   # per env step, on the launch stream (torch's current)
+    if getattr(tg, "trace", None):   # diagnostics (ILRL_DMA_TRACE=1): the chunks' timeline against the clock
+        print("dma-trace: " + json.dumps([(e, c, round((t - t0) * 1e3, 4)) for e, c, t in tg.trace] +
+                                         [("timed_end", 0, round(wall * 1e3, 4))]), file=sys.stderr, flush=True)
     if tg is not None and hasattr(tg, "close"):   # outside the timed region: unmap the peers' buffers (collective)
         tg.close()
     wall = _all_reduce(world, dev, a.backend, wall, dist.ReduceOp.MAX) if a.dist else wall
@@ -413,7 +435,7 @@ def run(a, world, rank, dev, n, precision, steps, warmup, phys, k=None):
         low_steps = float(sum(int((env._bench_acted[wlaunches + s] == N.HUM_AGENT_LOW).sum().item())
                               for s in range(launches)))
     elif a.hier:   # physics env-steps in the timed region: replay the same deterministic sequence and count them
-        low_steps = float(count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank))
+        low_steps = float(count_hier_low_steps(a, dev, n, precision, plan, wsizes, k, phys, rank))
         if a.dist:
             low_steps = _all_reduce(world, dev, a.backend, low_steps, dist.ReduceOp.SUM)   # all ranks
     return env, wall, kern_ms, low_steps, gather_s, gathered, sizes
@@ -428,7 +450,7 @@ def _all_reduce(world, dev, backend, x, op):
     return float(t.item())
 
 
-def count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank):
+def count_hier_low_steps(a, dev, n, precision, plan, wsizes, k, phys, rank):
     """Lanes that take a low-level (physics) step in each transition of the timed launches: a lane acts high next
     iff its last outputs carried the high-level obs (level hand-back, or done -> auto-reset)."""
     import torch
@@ -439,10 +461,11 @@ def count_hier_low_steps(a, dev, n, precision, sizes, wsizes, k, phys, rank):
     env.reset()
     expect_high = torch.ones(n, dtype=torch.bool, device=dev)
     low = 0
-    # the same launches as run(): warm-up launch w reads pool block w % 16, timed launch s block s % 16
-    seq = [(w, kk, False) for w, kk in enumerate(wsizes)] + [(s, kk, True) for s, kk in enumerate(sizes)]
-    for s, kk, timed in seq:
-        out = env.step_k(hpool[s % 16][:kk], pool[s % 16][:kk], autoreset=True)
+    # the same launches as run(): warm-up launch w reads pool block w % 16, timed launch (b, o, kk) rows o .. o + kk
+    # of block b % 16
+    seq = [(w, 0, kk, False) for w, kk in enumerate(wsizes)] + [(b, o, kk, True) for b, o, kk in plan]
+    for s, o, kk, timed in seq:
+        out = env.step_k(hpool[s % 16][o:o + kk], pool[s % 16][o:o + kk], autoreset=True)
         agents, done = out[0], out[5]
         for t in range(kk):
             if timed:
@@ -587,6 +610,7 @@ def main():
         np.savez(a.dump_gather, **{"%s_%d" % (nm, j): g[c].numpy() for j, g in enumerate(gathered)
                                    for c, nm in enumerate(names)})
     if rank == 0:
+        base, drain = launch_sizes(a.steps, a.k), getattr(a, "drain", None)   # the plan before the drain split
         total = n * world * a.steps
         phys_steps_per_step = (low_steps / world / a.steps) if a.hier else n   # per GPU, per env step
         value = (low_steps if a.hier else total) / wall_max
@@ -607,16 +631,18 @@ def main():
                                     if a.hier else "HumanoidBulletEnv-v0-Low step+reward, ") +
                                    "%s, %d envs/GPU, %s, auto-reset, %s env steps per %s" % (
                                        a.clip, n, _actions_desc(a),
-                                       "/".join(str(s) for s in sorted(set(sizes), reverse=True)),
+                                       "/".join(str(s) for s in sorted(set(base), reverse=True)),
                                        ("hum_hier_rollout_fused launch (both networks inside the env kernel)"
                                         if a.fused else
                                         "hum_hier_rollout call (2 policy launches + 1 env launch per transition)")
-                                       if a.hier and a.policy else "launch"),
+                                       if a.hier and a.policy else "launch") +
+                                   (" (the last launch's final %d steps run as a separate drain launch: the "
+                                    "trajectory gather's per-launch chunks, bench.launch_plan)" % drain if drain else ""),
                        "fused": bool(a.policy and a.fused),
                        "sample_batch_columns": bool(a.policy and a.sample_batch),
                        "envs_per_gpu": n, "clip": a.clip, "k": a.k, "terrain": a.terrain,
                        # the launches the timed region actually ran (--steps < k: one shorter launch)
-                       "launches": len(sizes), "steps_per_launch": max(sizes),
+                       "launches": len(sizes), "steps_per_launch": max(base),
                        "launch_sizes": sorted(set(sizes), reverse=True),
                        "parallelism": "lane-sharded x%d" % world, "block": a.block, "physics_overrides": phys},
             # per env step: kernel_ms = launch duration / k; achieved = the env step's algorithmic bytes over it
@@ -639,11 +665,13 @@ def main():
             out["agent_transitions_per_s"] = total / wall_max
         if a.dist and a.gather_every and not a.policy:
             out["gather"] = {"every": a.gather_every, "backend": a.backend, "to_rank": 0, "transport": a.transport,
-                             "op": ("rank 0 pulls every rank's packed lane-major fragment with the SDMA copy engines "
-                                    "(IPC-mapped buffers, parallel.DmaGather), asynchronous, double-buffered"
+                             "op": ("rank 0 pulls every launch's rows (one contiguous range of every rank's packed "
+                                    "step-major fragment) with the SDMA copy engines (IPC-mapped buffers, "
+                                    "parallel.DmaGather) while the next launch runs, double-buffered"
                                     if a.transport == "dma" else
-                                    "dist.gather of one packed lane-major fragment (RCCL point-to-point), "
+                                    "dist.gather of one packed step-major fragment (RCCL point-to-point), "
                                     "asynchronous, double-buffered") + "; completed inside the timed region",
+                             "drain_launch_steps": drain,
                              "host_seconds": gather_s, "bytes_per_rank_per_step": n * (70 * 4 + 17 * 4 + 4 + 1),
                              "fragments": -(-a.steps // a.gather_every)}
         if world == 1 and not a.no_secondary and not a.hier and not a.policy:

@@ -118,8 +118,15 @@ extern "C" int hum_dma_wait(hum_dma_ticket* ticket) {
     if (!ticket || !ticket->signal) return fail(HUM_ERR_ARG, "hum_dma_wait: no copy in flight");
     hsa_signal_t sig;
     sig.handle = ticket->signal;
-    const hsa_signal_value_t v =
-        hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    // a chunk's pull takes 0.05-1 ms: spin for up to ~2 ms (no interrupt wake-up on the gather's critical path at
+    // the end of a run), then sleep on the signal
+    static const uint64_t spin = [] {
+        uint64_t f = 0;
+        return hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f ? f / 500 : 0;
+    }();
+    hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, spin, HSA_WAIT_STATE_ACTIVE);
+    while (v >= 1)
+        v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
     hsa_signal_destroy(sig);
     ticket->signal = 0;
     if (v != 0) return fail(HUM_ERR_HIP, "hum_dma_wait: the copy engine reported an error");

@@ -12,6 +12,7 @@ import math
 import os
 import queue
 import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -86,13 +87,16 @@ class TrajectoryGather:
 
     * Static shapes: every rank's lane count is known from the sharding (`counts`, e.g. `shard`), so no count
       exchange and no host synchronisation happen per call.
-    * One packed, lane-major uint8 buffer per fragment: lane i's row holds its G steps of every field (raw bytes,
-      fields ordered by descending item size so each typed view is aligned).  `pack` writes a launch's
-      time-major outputs [k, n, ...] into the fragment's typed views - one strided device copy per field, the only
-      copy - and the whole fragment travels as ONE message.
-    * Asynchronous: `start` issues the gather (RCCL point-to-point sends to `dst`, `dist.gather`) ordered after the
-      packs on the current stream and returns; the next env launches proceed while it moves.  Fragments alternate
-      between `slots` buffers; packing into a slot first makes the stream wait for that slot's previous gather.
+    * One packed uint8 buffer per fragment, step-major: step t's block (`SB` bytes) holds that step's rows of every
+      field for the `m` (largest shard's) lanes - [m, 70] obs, then [m, 17] actions, ... (raw bytes, fields ordered by
+      descending item size, each field's rows 8-byte aligned).  So the steps [t0, t1) one env launch produced are ONE
+      contiguous byte range, which can travel as soon as that launch is packed (DmaGather's per-launch chunks), and
+      `pack` is one hum_pack_rows launch (every field's time-major [k, n, ...] outputs into their rows, the only copy).
+    * Asynchronous: `commit(slot, t0, t1, final)` after each pack; the fragment's gather (RCCL point-to-point sends to
+      `dst`, `dist.gather`) is issued on the final one, ordered after the packs on the current stream, and returns; the
+      next env launches proceed while it moves.  Fragments alternate between `slots` buffers; packing into a slot
+      first waits for that slot's previous gather.
+    * `result` presents the gathered fragment lane-major, {field: [sum n_r, G, ...]} (RLlib's per-env rows).
     * gloo (CPU tests): the same layout, gathered synchronously through host memory.
     """
 
@@ -105,26 +109,29 @@ class TrajectoryGather:
         self.counts, self.G, self.dst, self.dev = [int(c) for c in counts], int(G), dst, torch.device(device)
         self.n, self.m = self.counts[self.rank], max(self.counts)
         self.nccl = self.on and dist.get_backend() == "nccl"
-        self.fields = []   # (name, per-step trailing shape, dtype, byte offset in the row, bytes per step)
+        self.fields = []   # (name, per-step trailing shape, dtype, byte offset in the step block, bytes per lane-step)
         off = 0
         for name, shape, dtype in sorted(fields, key=lambda f: -torch.empty(0, dtype=f[2]).element_size()):
             isz = torch.empty(0, dtype=dtype).element_size()
             w = int(math.prod(shape)) * isz
             self.fields.append((name, tuple(shape), dtype, off, w))
-            off += self.G * w
+            off += -(-(self.m * w) // 8) * 8
         self.order = [f[0] for f in fields]
-        self.W = -(-off // 8) * 8   # row width: a multiple of the largest item size
-        self.send = [torch.zeros((self.m, self.W), dtype=torch.uint8, device=self.dev) for _ in range(slots)]
-        self.recv = [[torch.empty((self.m, self.W), dtype=torch.uint8, device=self.dev if self.nccl else "cpu")
+        self.SB = off                 # bytes per step block (a multiple of 8)
+        self.W = sum(f[4] for f in self.fields)   # payload bytes per lane-step
+        self.bytes = self.G * self.SB
+        self.send = [torch.zeros(self.bytes, dtype=torch.uint8, device=self.dev) for _ in range(slots)]
+        self.recv = [[torch.empty(self.bytes, dtype=torch.uint8, device=self.dev if self.nccl else "cpu")
                       for _ in range(self.world)] if self.rank == dst else None for _ in range(slots)]
         self.work = [None] * slots
         self.fragments = 0
 
     def _view(self, buf, name, rows=None):
+        """Time-major typed view [G, rows (default m), ...] of one field in a fragment buffer."""
         for nm, shape, dtype, off, w in self.fields:
             if nm == name:
-                b = buf[:rows] if rows is not None else buf
-                return b[:, off:off + self.G * w].view(dtype).view((b.shape[0], self.G) + shape)
+                v = buf.view(self.G, self.SB)[:, off:off + self.m * w].view(dtype).unflatten(1, (self.m,) + shape)
+                return v[:, :rows] if rows is not None else v
         raise KeyError(name)
 
     def pack(self, slot, t0, outputs):
@@ -139,13 +146,16 @@ class TrajectoryGather:
         k = ks.pop()
         if t0 < 0 or t0 + k > self.G:
             raise ValueError("pack: steps [%d, %d) cross the fragment of %d steps" % (t0, t0 + k, self.G))
-        if self.work[slot] is not None:   # the slot's previous gather must have read the buffer
-            self.work[slot].wait()
-            self.work[slot] = None
+        self._wait_slot(slot, t0)
         if self.dev.type == "cuda":
             return self._pack_native(slot, t0, outputs)
         for name, x in outputs.items():
-            self._view(self.send[slot], name, self.n)[:, t0:t0 + x.shape[0]].copy_(x.transpose(0, 1))
+            self._view(self.send[slot], name, self.n)[t0:t0 + x.shape[0]].copy_(x)
+
+    def _wait_slot(self, slot, t0):
+        if self.work[slot] is not None:   # the slot's previous gather must have read the buffer
+            self.work[slot].wait()
+            self.work[slot] = None
 
     def _pack_native(self, slot, t0, outputs):
         import ctypes
@@ -162,9 +172,15 @@ class TrajectoryGather:
             isz = x.element_size()
             arr[j].src, arr[j].dst = x.data_ptr(), base + off
             arr[j].src_step, arr[j].src_lane = x.stride(0) * isz, x.stride(1) * isz
-            arr[j].dst_step, arr[j].dst_lane, arr[j].row_bytes = w, self.W, w
+            arr[j].dst_step, arr[j].dst_lane, arr[j].row_bytes = self.SB, w, w
         stream = torch.cuda.current_stream(self.dev).cuda_stream
         N.check(N.lib().hum_pack_rows(arr, len(outputs), kk, self.n, t0, ctypes.c_void_p(stream)), "hum_pack_rows")
+
+    def commit(self, slot, t0, t1, final):
+        """Steps [t0, t1) of slot's fragment are packed; `final`: the fragment is complete (or the run ends) - gather
+        it.  (The collective transport moves whole fragments; DmaGather moves every committed range at once.)"""
+        if final:
+            self.start(slot)
 
     def start(self, slot):
         """Gather slot's packed fragment onto dst (asynchronous on RCCL)."""
@@ -185,11 +201,12 @@ class TrajectoryGather:
                 self.work[j] = None
 
     def result(self, slot):
-        """dst: the gathered fragment as {field: [sum n_r, G, ...]} in rank order (after wait); None elsewhere."""
+        """dst: the gathered fragment lane-major, {field: [sum n_r, G, ...]} in rank order (after wait); None
+        elsewhere."""
         if self.recv[slot] is None:
             return None
-        full = torch.cat([r[:c] for r, c in zip(self.recv[slot], self.counts)], dim=0)
-        return {nm: self._view(full, nm) for nm in self.order}
+        return {nm: torch.cat([self._view(r, nm, c) for r, c in zip(self.recv[slot], self.counts)],
+                              dim=1).transpose(0, 1).contiguous() for nm in self.order}
 
 
 class DmaUnavailable(RuntimeError):
@@ -205,12 +222,15 @@ class DmaGather(TrajectoryGather):
 
     * Setup (collective, once): every rank exports its `slots` packed send buffers (hum_ipc_export); the handles are
       all-gathered over a gloo control group; the learner rank maps every peer's buffers (hum_ipc_open).
-    * Per fragment: pack as TrajectoryGather (one hum_pack_rows launch per env launch), then `start` records an event
-      on the packing stream and hands the fragment to a helper thread - the main thread goes on launching.  A
-      sender's helper waits for its event, tells the learner "fragment f is packed" over the control group and waits
-      for the learner's "pulled"; the learner's helper waits for its own event, then for each sender's "packed"
-      issues an SDMA pull of that sender's fragment (hum_dma_copy; engines round-robin), waits for all of them and
-      answers "pulled".  A slot is packed again only after its previous fragment was pulled.
+    * Per env launch (a chunk): pack as TrajectoryGather (one hum_pack_rows launch), then `commit` records an event
+      on the packing stream and hands the chunk - the launch's steps [t0, t1), one contiguous byte range of the
+      step-major fragment - to a helper thread; the main thread goes on launching.  A sender's helper waits for its
+      event, tells the learner "chunk c is packed" over the control group and waits for the learner's "pulled"; the
+      learner's helper waits for its own event, then for each sender's "packed" issues an SDMA pull of that sender's
+      range (hum_dma_copy; engines round-robin), waits for all of them and answers "pulled".  So a launch's rows move
+      while the next launch computes, and what is still in flight when the last launch ends is that launch's rows
+      only (bench.py ends a gathering run with a short drain launch).  A slot is packed again (t0 = 0) only after
+      its previous fragment's last chunk was pulled.
     * The control messages are 8-byte host tensors on their own gloo group, used by the helper threads only.
     Same layout and result() as TrajectoryGather; `transport` names it in the bench line."""
 
@@ -221,7 +241,7 @@ class DmaGather(TrajectoryGather):
         if not (self.on and self.dev.type == "cuda"):
             raise ValueError("DmaGather needs an initialised process group and device buffers")
         if self.rank == dst:   # the learner's receive buffers live on its device whatever the default group's backend
-            self.recv = [[torch.empty((self.m, self.W), dtype=torch.uint8, device=self.dev) for _ in range(self.world)]
+            self.recv = [[torch.empty(self.bytes, dtype=torch.uint8, device=self.dev) for _ in range(self.world)]
                          for _ in range(slots)]
         from . import _native as N
         self.N = N
@@ -256,7 +276,7 @@ class DmaGather(TrajectoryGather):
                         src = self.send[j].data_ptr() if r == dst else self.remote[r][j][0]
                         t = N.HumDmaTicket()
                         N.check(L.hum_dma_copy(ctypes.c_void_p(self.recv[j][r].data_ptr()), ctypes.c_void_p(src),
-                                               min(256, self.m * self.W), r, ctypes.byref(t)), "hum_dma_copy")
+                                               min(256, self.bytes), r, ctypes.byref(t)), "hum_dma_copy")
                         N.check(L.hum_dma_wait(ctypes.byref(t)), "hum_dma_wait")
             except Exception as e:   # noqa: BLE001 - reported to every rank below
                 err = repr(e)
@@ -269,34 +289,46 @@ class DmaGather(TrajectoryGather):
         self.free = [threading.Event() for _ in range(slots)]   # the slot's last fragment has been pulled
         for e in self.free:
             e.set()
+        self.chunks = 0
+        self.trace = [] if os.environ.get("ILRL_DMA_TRACE") == "1" else None   # diagnostics: per-chunk timestamps
         self.jobs = queue.Queue()
         self.err = []
         self.thread = threading.Thread(target=self._helper, name="dma-gather", daemon=True)
         self.thread.start()
 
-    def pack(self, slot, t0, outputs):
-        if not self.free[slot].is_set():
+    def _wait_slot(self, slot, t0):
+        if t0 == 0 and not self.free[slot].is_set():   # a new fragment: the slot's previous one must be pulled
             self._wait_free(slot)
-        return super().pack(slot, t0, outputs)
 
     def _wait_free(self, slot):
         while not self.free[slot].wait(0.05):
             if self.err:
                 raise RuntimeError("DmaGather helper failed: %s" % self.err[0])
 
-    def start(self, slot):
-        self.fragments += 1
+    def commit(self, slot, t0, t1, final):
+        if not 0 <= t0 < t1 <= self.G:
+            raise ValueError("commit: steps [%d, %d) outside the fragment of %d steps" % (t0, t1, self.G))
+        if t0 == 0:
+            self.free[slot].clear()
+        if final:
+            self.fragments += 1
+        self.chunks += 1
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.dev))
-        self.free[slot].clear()
-        self.jobs.put((self.fragments, slot, ev))
+        if self.trace is not None:
+            self.trace.append(("commit", self.chunks, time.perf_counter()))
+        self.jobs.put((self.chunks, slot, t0, t1, final, ev))
+
+    def start(self, slot):
+        """The whole fragment as one chunk."""
+        self.commit(slot, 0, self.G, True)
 
     def wait(self, slot=None):
         for j in range(len(self.free)) if slot is None else [slot]:
             self._wait_free(j)
 
     def _helper(self):
-        """The transfer loop (one fragment per job).  A failure on any rank is passed on as a negative message, so
+        """The transfer loop (one chunk per job).  A failure on any rank is passed on as a negative message, so
         every rank's helper stops and its main thread raises from pack / wait instead of waiting forever."""
         L = self.N.lib()
         msg = torch.zeros(1, dtype=torch.int64)
@@ -306,48 +338,64 @@ class DmaGather(TrajectoryGather):
                 job = self.jobs.get()
                 if job is None:
                     return
-                f, slot, ev = job
+                c, slot, t0, t1, final, ev = job
+                lo, nbytes = t0 * self.SB, (t1 - t0) * self.SB
                 if self.rank != self.dst:
                     try:
                         ev.synchronize()
                     except Exception:
                         send(-1, self.dst)
                         raise
-                    send(f, self.dst)                           # packed
+                    send(c, self.dst)                           # packed
                     dist.recv(msg, self.dst, group=self.ctrl)   # pulled
-                    if int(msg.item()) != f:
-                        raise RuntimeError("fragment %d: the learner answered %d" % (f, int(msg.item())))
+                    if int(msg.item()) != c:
+                        raise RuntimeError("chunk %d: the learner answered %d" % (c, int(msg.item())))
                 else:
-                    tickets = []
+                    tickets, posted = [], {}
+                    tr = self.trace
                     try:
+                        # every sender's "packed" is posted at once (the senders finish the launch together: the
+                        # waits overlap instead of adding up), then each pull is issued as its message is in
+                        peers = [r for r in range(self.world) if r != self.dst]
+                        msgs = {r: torch.zeros(1, dtype=torch.int64) for r in peers}
+                        posted = {r: dist.irecv(msgs[r], r, group=self.ctrl) for r in peers}
                         ev.synchronize()
-                        for r in range(self.world):
-                            if r == self.dst:   # its own fragment: also a copy-engine transfer
+                        if tr is not None:
+                            tr.append(("packed", c, time.perf_counter()))
+                        for r in [self.dst] + peers:
+                            if r == self.dst:   # its own rows: also a copy-engine transfer
                                 src_ptr = self.send[slot].data_ptr()
                             else:
-                                dist.recv(msg, r, group=self.ctrl)
-                                if int(msg.item()) != f:
-                                    raise RuntimeError("rank %d sent %d for fragment %d" % (r, int(msg.item()), f))
+                                posted.pop(r).wait()
+                                if int(msgs[r].item()) != c:
+                                    raise RuntimeError("rank %d sent %d for chunk %d" % (r, int(msgs[r].item()), c))
                                 src_ptr = self.remote[r][slot][0]
                             if self.counts[r]:
                                 t = self.N.HumDmaTicket()
-                                self.N.check(L.hum_dma_copy(ctypes.c_void_p(self.recv[slot][r].data_ptr()),
-                                                            ctypes.c_void_p(src_ptr), self.counts[r] * self.W,
-                                                            len(tickets), ctypes.byref(t)), "hum_dma_copy")
+                                self.N.check(L.hum_dma_copy(ctypes.c_void_p(self.recv[slot][r].data_ptr() + lo),
+                                                            ctypes.c_void_p(src_ptr + lo), nbytes, len(tickets),
+                                                            ctypes.byref(t)), "hum_dma_copy")
                                 tickets.append(t)
+                        if tr is not None:
+                            tr.append(("issued", c, time.perf_counter()))
                         while tickets:
                             self.N.check(L.hum_dma_wait(ctypes.byref(tickets.pop(0))), "hum_dma_wait")
+                        if tr is not None:
+                            tr.append(("pulled", c, time.perf_counter()))
                     except Exception:
                         for t in tickets:   # retire the copies in flight before giving up
                             L.hum_dma_wait(ctypes.byref(t))
+                        for w in posted.values():   # the senders' messages still posted
+                            w.wait()
                         for r in range(self.world):
                             if r != self.dst:
                                 send(-1, r)
                         raise
-                    for r in range(self.world):
-                        if r != self.dst:
-                            send(f, r)                          # pulled
-                self.free[slot].set()
+                    done = torch.tensor([c], dtype=torch.int64)
+                    for w in [dist.isend(done, r, group=self.ctrl) for r in range(self.world) if r != self.dst]:
+                        w.wait()                                # pulled
+                if final:
+                    self.free[slot].set()
         except Exception as e:   # surfaced on the main thread by pack / wait
             self.err.append(repr(e))
 

@@ -88,6 +88,26 @@ def test_bench_launch_sizes_cover_exactly_the_requested_steps():
     assert bench.launch_sizes(0, 32) == []
 
 
+def test_bench_drain_plan_replays_the_same_action_rows():
+    """bench.launch_plan(drain=True) (the chunked copy-engine gather): the last launch's final fifth runs as its own
+    launch over the SAME rows of the same action block, so the trajectory is the unsplit plan's; every launch stays
+    inside one block of k rows (and so inside one gather fragment, G a multiple of k)."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    assert bench.launch_plan(20, 32, drain=True) == [(0, 0, 16), (0, 16, 4)]
+    assert bench.launch_plan(1000, 32, drain=True)[-3:] == [(30, 0, 32), (31, 0, 6), (31, 6, 2)]
+    assert bench.launch_plan(1, 32, drain=True) == [(0, 0, 1)]
+    for steps in (1, 2, 7, 20, 31, 32, 33, 100, 1000):
+        for k in (1, 8, 32, 64):
+            base = bench.launch_plan(steps, k)
+            assert [kk for _, _, kk in base] == bench.launch_sizes(steps, k)
+            plan = bench.launch_plan(steps, k, drain=True)
+            rows = [(b, r) for b, o, kk in plan for r in range(o, o + kk)]
+            assert rows == [(b, r) for b, o, kk in base for r in range(o, o + kk)]
+            assert all(0 <= o and o + kk <= k and kk > 0 for _, o, kk in plan)
+
+
 def test_register_envs_vectorised_by_default(monkeypatch):
     """register_envs() registers the N-lane creators by default (one launch per sampler step for all of a worker's
     envs): HumanoidBulletEnv-v0-Low -> make_env_low_vec, HumanoidBulletEnv-v0-Hier -> make_env_hier_vec; with
