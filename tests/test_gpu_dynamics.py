@@ -1,0 +1,85 @@
+"""The HIP kernel's multibody dynamics against first principles (GPU).
+
+tests/test_oracle_dynamics.py pins the oracle's dynamics core to Newtonian mechanics; this file applies the laws
+that need no oracle arithmetic to the kernel itself, through the C-ABI (hum_set_state / hum_step / hum_get_state),
+with Bullet's link damping, the MJCF joint damping and self-collision switched off in hum_config and every lane
+5 m above the plane (no contacts) with its joints inside their ranges (no limit rows):
+
+* free fall: released at rest with zero actions, after the env step's 4 substeps z = z0 - 10 g dt^2 and
+  vz = -4 g dt, every other coordinate unchanged - exactly in fp64, to float rounding in fp32;
+* free motion, one substep (hum_config substeps = 1): the kernel's accelerations (nu' - nu) / dt conserve linear
+  and angular momentum and satisfy the power balance dT/dt = tau . qd, with the mass matrix and its rate from the
+  model (oracle.mass_matrix: the Jacobian-summed H, independent of the kernel's articulated-body recursion).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+import test_oracle_dynamics as D  # noqa: E402
+from ilrl_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+O = D.O
+DT = 0.0165 / 4
+FREE = dict(lin_damp=0.0, ang_damp=0.0, joint_damping=0, self_collision=0)
+
+
+def _env(n, precision, **kw):
+    env = HumanoidVecEnv(n, seed=3, precision=precision, **FREE, **kw)
+    env.reset()
+    return env
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_kernel_free_fall_is_exact(precision):
+    n = 64
+    env = _env(n, precision)
+    rng = np.random.default_rng(5)
+    env.set_state(phys=np.array([D.random_state(rng, moving=False) for _ in range(n)]))
+    s0, _ = env.get_state()   # the state as the kernel holds it (rounded to float for fp32)
+    env.step(np.zeros((n, 17), np.float32), autoreset=False)
+    s1, _ = env.get_state()
+    env.close()
+    tol_z, tol = (1e-12, 1e-12) if precision == "fp64" else (4e-6, 2e-6)
+    assert np.abs(s1[:, 2] - (s0[:, 2] - 10 * D.G * DT * DT)).max() < tol_z
+    assert np.abs(s1[:, 9] + 4 * D.G * DT).max() < tol
+    np.testing.assert_allclose(s1[:, 0:2], s0[:, 0:2], rtol=0, atol=tol)
+    np.testing.assert_allclose(s1[:, 7:9], 0, atol=tol)
+    np.testing.assert_allclose(s1[:, 10:13], 0, atol=tol)
+    np.testing.assert_allclose(s1[:, 13:30], s0[:, 13:30], rtol=0, atol=tol)
+    np.testing.assert_allclose(s1[:, 30:47], 0, atol=100 * tol)
+    sign = np.where(np.sum(s1[:, 3:7] * s0[:, 3:7], axis=1) < 0, -1.0, 1.0)[:, None]
+    np.testing.assert_allclose(s1[:, 3:7] * sign, s0[:, 3:7], rtol=0, atol=tol)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_kernel_free_motion_conserves_momentum_and_balances_power(precision):
+    n = 32
+    env = _env(n, precision, substeps=1, dt_env=DT, gravity=0.0)
+    rng = np.random.default_rng(9)
+    env.set_state(phys=np.array([D.random_state(rng) for _ in range(n)]))
+    s0, _ = env.get_state()
+    act = rng.uniform(-1, 1, (n, 17)).astype(np.float32)
+    act[: n // 2] = 0   # half the lanes coast (tau = 0), half are driven
+    env.step(act, autoreset=False)
+    s1, _ = env.get_state()
+    env.close()
+    rel = 1e-7 if precision == "fp64" else 2e-3
+    h = 1e-6
+    for i in range(n):
+        tau = O.motor_torques(act[i].astype(np.float64))
+        nu0, acc = D.nu_of(s0[i]), (D.nu_of(s1[i]) - D.nu_of(s0[i])) / DT
+        H = O.mass_matrix(s0[i])
+        Hd = (O.mass_matrix(D.advance(s0[i], h)) - O.mass_matrix(D.advance(s0[i], -h))) / (2 * h)
+        pd = H @ acc + Hd @ nu0
+        P = (H @ nu0)[3:6]
+        Ld = pd[0:3] + np.cross(s0[i, 7:10], P) + np.cross(s0[i, 0:3], pd[3:6])
+        Td = nu0 @ H @ acc + 0.5 * nu0 @ Hd @ nu0
+        power = tau @ s0[i, 30:47]
+        assert abs(Td - power) < rel * (abs(nu0 @ H @ acc) + abs(power)), (i, Td, power)
+        assert np.abs(pd[3:6]).max() < rel * np.abs(H[3:6] @ acc).max(), (i, pd[3:6])
+        assert np.abs(Ld).max() < 10 * rel * (np.abs(H[0:3] @ acc).max() + np.abs(np.cross(s0[i, 0:3], H[3:6] @ acc)).max()), (i, Ld)
