@@ -9,7 +9,9 @@ with Bullet's link damping, the MJCF joint damping and self-collision switched o
   vz = -4 g dt, every other coordinate unchanged - exactly in fp64, to float rounding in fp32;
 * free motion, one substep (hum_config substeps = 1): the kernel's accelerations (nu' - nu) / dt conserve linear
   and angular momentum and satisfy the power balance dT/dt = tau . qd, with the mass matrix and its rate from the
-  model (oracle.mass_matrix: the Jacobian-summed H, independent of the kernel's articulated-body recursion).
+  model (oracle.mass_matrix: the Jacobian-summed H, independent of the kernel's articulated-body recursion);
+* constraint impulses, one substep (self-collision on where limbs overlap, joints past their limits elsewhere): no
+  net force from self-contacts and limit rows, no net torque from limit rows.
 """
 import numpy as np
 import pytest
@@ -83,3 +85,49 @@ def test_kernel_free_motion_conserves_momentum_and_balances_power(precision):
         assert abs(Td - power) < rel * (abs(nu0 @ H @ acc) + abs(power)), (i, Td, power)
         assert np.abs(pd[3:6]).max() < rel * np.abs(H[3:6] @ acc).max(), (i, pd[3:6])
         assert np.abs(Ld).max() < 10 * rel * (np.abs(H[0:3] @ acc).max() + np.abs(np.cross(s0[i, 0:3], H[3:6] @ acc)).max()), (i, Ld)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_kernel_limit_and_self_contact_impulses_are_internal(precision):
+    """One substep of the kernel with no gravity, 5 m up: lanes whose limbs overlap (self-collision on) and lanes
+    with joints past their limits.  The constraint impulse H(q0) (nu' - nu_free) (nu_free = nu0 + dt aba from the
+    model) has no net force, and for the limit-only lanes no net torque either: the rows act between parts of the
+    body or along a joint axis."""
+    n = 16
+    rng = np.random.default_rng(13)
+    P = D.params(gravity=0.0)
+    P.self_collision = 1
+    states, kinds = [], []
+    for i in range(n):
+        if i % 2 == 0:
+            states.append(D._self_contact_state(rng))
+            kinds.append("self")
+        else:
+            while True:   # limits only: a pose with no overlapping limbs
+                st = D.random_state(rng)
+                j = rng.choice(17, 4, replace=False)
+                st[13 + j[:2]] = O.LO[j[:2]] - 0.02
+                st[30 + j[:2]] = -np.abs(st[30 + j[:2]]) - 0.5
+                st[13 + j[2:]] = O.HI[j[2:]] + 0.02
+                st[30 + j[2:]] = np.abs(st[30 + j[2:]]) + 0.5
+                if len(O.contacts(st, P)) == 0:
+                    break
+            states.append(st)
+            kinds.append("limit")
+    env = HumanoidVecEnv(n, seed=3, precision=precision, lin_damp=0.0, ang_damp=0.0, joint_damping=0,
+                         self_collision=1, substeps=1, dt_env=DT, gravity=0.0)
+    env.reset()
+    env.set_state(phys=np.array(states))
+    s0, _ = env.get_state()
+    env.step(np.zeros((n, 17), np.float32), autoreset=False)
+    s1, _ = env.get_state()
+    env.close()
+    rel = 1e-9 if precision == "fp64" else 2e-3
+    for i in range(n):
+        nu_free = D.nu_of(s0[i]) + DT * O.aba(s0[i], np.zeros(17), P)
+        imp = O.mass_matrix(s0[i]) @ (D.nu_of(s1[i]) - nu_free)
+        scale = np.abs(imp).max()
+        assert scale > 1e-3, (i, kinds[i])
+        assert np.abs(imp[3:6]).max() < rel * scale, (i, kinds[i], imp[3:6], scale)
+        if kinds[i] == "limit":
+            assert np.abs(imp[0:3]).max() < rel * scale, (i, imp[0:3], scale)

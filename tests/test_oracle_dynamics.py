@@ -18,7 +18,11 @@ reference's XML) and the oracle's forward kinematics (`om_link_frames`):
   balance dT/dt = tau . qd + g . P holds;
 * one substep without contacts or limits is semi-implicit Euler of the ABA (velocities first, then positions, the
   base orientation by the exponential map), and a body released at rest free-falls exactly: z_n = z0 - g dt^2
-  n(n+1)/2.
+  n(n+1)/2;
+* the constraint rows' impulses (H(q0) (nu' - nu_free) after one substep): joint-limit impulses act on the violated
+  joints only, push them back into range, stay within limit_max_impulse and leave both momenta alone; self-contact
+  impulses are equal and opposite (no net force); the ground only pushes (net impulse up) and its horizontal part
+  stays inside the friction box's bound sqrt(2) mu times the vertical part.
 
 Bullet's link damping (0.04, default on) and MJCF joint damping are switched off where a conservation law is
 checked; contact, limit and damping semantics stay hypotheses about Bullet.  The GPU kernel
@@ -266,3 +270,83 @@ def test_default_damping_only_dissipates():
         T.append(0.5 * nu @ O.mass_matrix(st) @ nu)
         st = O.phys_step(st, np.zeros(17), P)
     assert all(b < a for a, b in zip(T, T[1:])), T
+
+
+def _constraint_impulse(st, P):
+    """One substep of the oracle; returns (H(q0) (nu1 - nu_free), contacts): the generalised impulse the constraint
+    rows (limits, contacts) applied, nu_free = nu0 + dt aba being the velocity before the constraint phase."""
+    P.nsub = 1
+    nu_free = nu_of(st) + P.dt * O.aba(st, np.zeros(17), P)
+    out = O.phys_step(st, np.zeros(17), P)
+    return O.mass_matrix(st) @ (nu_of(out) - nu_free), O.contacts(st, P)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_limit_impulses_are_internal_and_act_on_their_joints_only(seed):
+    """Joints pushed past their limits (moving further out), no gravity / contacts: the limit rows' impulse is
+    e_j lambda_j on the violated joints only - pushing back into range, at most limit_max_impulse - and moves
+    neither the linear nor the angular momentum of the body."""
+    rng = np.random.default_rng(700 + seed)
+    st = random_state(rng)
+    lo_j, hi_j = rng.choice(17, 6, replace=False).reshape(2, 3)
+    st[13 + lo_j] = O.LO[lo_j] - rng.uniform(0.005, 0.03, 3)
+    st[13 + hi_j] = O.HI[hi_j] + rng.uniform(0.005, 0.03, 3)
+    st[30 + lo_j] = -np.abs(st[30 + lo_j])
+    st[30 + hi_j] = np.abs(st[30 + hi_j])
+    P = params(gravity=0.0)
+    imp, con = _constraint_impulse(st, P)
+    assert len(con) == 0
+    scale = np.abs(imp).max()
+    assert scale > 1e-3
+    assert np.abs(imp[0:6]).max() < 1e-10 * scale
+    others = np.setdiff1d(np.arange(17), np.concatenate([lo_j, hi_j]))
+    assert np.abs(imp[6 + others]).max() < 1e-10 * scale
+    # a row's impulse is >= 0 (it may end at 0 when the other rows' impulses already turned the joint around)
+    assert (imp[6 + lo_j] > -1e-12 * scale).all() and (imp[6 + hi_j] < 1e-12 * scale).all()
+    assert np.abs(imp[6:]).max() <= P.limit_max_impulse * (1 + 1e-12)
+
+
+def _self_contact_state(rng):
+    P = params()
+    P.self_collision = 1
+    for _ in range(2000):
+        st = random_state(rng)
+        st[13:30] = rng.uniform(O.LO + 1e-3, O.HI - 1e-3)   # any pose in range: limbs often cross each other
+        con = O.contacts(st, P)
+        if len(con) >= 2 and (con[:, 2] < 0).any():   # at least one pair overlapping (not only speculative)
+            return st
+    raise AssertionError("no self-contact pose found")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_self_contact_impulses_conserve_linear_momentum(seed):
+    """Self-collision contacts (geom pairs of the same body) apply equal and opposite impulses: with no gravity and
+    the ground far below, the constraint impulse's base force rows vanish (Newton's third law through the
+    contact rows' Jacobians, normal and friction rows alike)."""
+    rng = np.random.default_rng(800 + seed)
+    st = _self_contact_state(rng)
+    P = params(gravity=0.0)
+    P.self_collision = 1
+    imp, con = _constraint_impulse(st, P)
+    assert len(con) >= 2 and (con[:, 1] >= 0).all()
+    scale = np.abs(imp).max()
+    assert scale > 1e-4
+    assert np.abs(imp[3:6]).max() < 1e-10 * scale
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ground_impulses_push_up_within_the_friction_cone(seed):
+    """Falling onto the plane (gravity on, lowest part 1 cm into it, moving down and sideways): the ground's net
+    impulse points up (normal rows clamped at >= 0) and its horizontal part is bounded by sqrt(2) mu times its
+    vertical part (each contact's two friction rows are clamped to mu times that contact's final normal impulse)."""
+    rng = np.random.default_rng(900 + seed)
+    st = random_state(rng, z=0.0)
+    st[2] -= O.parts(st)[:32, 2].min() + 0.01
+    st[7:10] = [rng.uniform(-1, 1), rng.uniform(-1, 1), -1.0]
+    P = params(gravity=G)
+    imp, con = _constraint_impulse(st, P)
+    assert len(con) >= 1 and (con[:, 1] < 0).all()
+    J = imp[3:6]
+    assert J[2] > 0.1
+    mu = P.mu_ground
+    assert np.hypot(J[0], J[1]) <= np.sqrt(2) * mu * J[2] * (1 + 1e-9)
