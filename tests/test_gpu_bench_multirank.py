@@ -42,9 +42,9 @@ def _port():
                          [(2, 2048, 8, 8, 16, 1, "gloo", "collective"), (8, 4096, 32, 32, 32, 61, "gloo", "collective"),
                           (1, 4096, 32, 32, 64, 7, "nccl", "collective"), (2, 2048, 8, 8, 32, 1, "gloo", "dma"),
                           (8, 4096, 32, 32, 64, 61, "gloo", "dma"), (1, 4096, 32, 32, 64, 7, "nccl", "dma"),
-                          (2, 2048, 8, 8, 16, 1, "gloo", "dma_fallback")],
+                          (2, 2048, 8, 8, 16, 1, "gloo", "dma_fallback"), (2, 2048, 8, 16, 32, 1, "gloo", "dma")],
                          ids=["2x2048", "config4_8x4096", "rccl_1x4096", "dma_2x2048", "dma_config4_8x4096",
-                              "dma_rccl_1x4096", "dma_fallback_2x2048"])
+                              "dma_rccl_1x4096", "dma_fallback_2x2048", "dma_2x2048_two_launches_per_fragment"])
 def test_bench_ranks_gather_equals_single_handle(tmp_path, ranks, lanes, k, every, steps, stride, backend, transport):
     """transport "dma": the default for N > 1 - IPC-mapped send buffers pulled by rank 0 with the SDMA copy engines
     (parallel.DmaGather; on one GPU the copies are intra-device, between GPUs they cross xGMI)."""
