@@ -70,7 +70,7 @@ def test_kernel_free_motion_conserves_momentum_and_balances_power(precision):
     env.step(act, autoreset=False)
     s1, _ = env.get_state()
     env.close()
-    rel = 1e-7 if precision == "fp64" else 2e-3
+    rel = 1e-7 if precision == "fp64" else 3e-4   # measured worst: 1.2e-9 / 2.7e-5 (tools/dyn_margins.py)
     h = 1e-6
     for i in range(n):
         tau = O.motor_torques(act[i].astype(np.float64))
