@@ -22,7 +22,9 @@ reference's XML) and the oracle's forward kinematics (`om_link_frames`):
 * the constraint rows' impulses (H(q0) (nu' - nu_free) after one substep): joint-limit impulses act on the violated
   joints only, push them back into range, stay within limit_max_impulse and leave both momenta alone; self-contact
   impulses are equal and opposite (no net force); the ground only pushes (net impulse up) and its horizontal part
-  stays inside the friction box's bound sqrt(2) mu times the vertical part.
+  stays inside the friction box's bound sqrt(2) mu times the vertical part;
+* over 0.1 s of free tumbling the energy and momentum drift halves with every halving of dt (first-order
+  consistency of the substep).
 
 Bullet's link damping (0.04, default on) and MJCF joint damping are switched off where a conservation law is
 checked; contact, limit and damping semantics stay hypotheses about Bullet.  The GPU kernel
@@ -350,3 +352,30 @@ def test_ground_impulses_push_up_within_the_friction_cone(seed):
     assert J[2] > 0.1
     mu = P.mu_ground
     assert np.hypot(J[0], J[1]) <= np.sqrt(2) * mu * J[2] * (1 + 1e-9)
+
+
+@pytest.mark.parametrize("seed", [40, 41, 44])
+def test_integrator_drift_is_first_order(seed):
+    """Free tumbling motion for 0.1 s (no gravity, torques, damping or contacts; joint rates small enough that no
+    limit is reached) at dt, dt/2, dt/4, dt/8: the drift of the kinetic energy and of the linear momentum halves
+    with every halving of dt - the substep is a consistent first-order integrator of the conserving dynamics
+    (semi-implicit Euler).  (Seeds whose drift is far above rounding at dt/8.)"""
+    st0 = random_state(np.random.default_rng(seed))
+    st0[30:47] *= 0.25
+    H0, nu0 = O.mass_matrix(st0), nu_of(st0)
+    E0, P0 = 0.5 * nu0 @ H0 @ nu0, (H0 @ nu0)[3:6]
+    dE, dP = [], []
+    for div in (1, 2, 4, 8):
+        P = params(gravity=0.0)
+        P.dt, P.nsub = 0.0165 / 4 / div, 1
+        st = st0.copy()
+        for _ in range(int(round(0.1 / P.dt))):
+            st = O.phys_step(st, np.zeros(17), P)
+            assert ((st[13:30] >= O.LO) & (st[13:30] <= O.HI)).all()
+        H, nu = O.mass_matrix(st), nu_of(st)
+        dE.append(abs(0.5 * nu @ H @ nu - E0) / E0)
+        dP.append(np.abs((H @ nu)[3:6] - P0).max())
+    for d in (dE, dP):
+        assert d[-1] > 1e-9
+        for a, b in zip(d, d[1:]):
+            assert 1.8 < a / b < 2.2, d
