@@ -11,7 +11,8 @@ with Bullet's link damping, the MJCF joint damping and self-collision switched o
   and angular momentum and satisfy the power balance dT/dt = tau . qd, with the mass matrix and its rate from the
   model (oracle.mass_matrix: the Jacobian-summed H, independent of the kernel's articulated-body recursion);
 * constraint impulses, one substep (self-collision on where limbs overlap, joints past their limits elsewhere): no
-  net force from self-contacts and limit rows, no net torque from limit rows.
+  net force from self-contacts and limit rows, no net torque from limit rows;
+* static equilibrium (default physics): lying on the plane after 6.6 s, the ground carries the weight.
 """
 import numpy as np
 import pytest
@@ -131,3 +132,28 @@ def test_kernel_limit_and_self_contact_impulses_are_internal(precision):
         assert np.abs(imp[3:6]).max() < rel * scale, (i, kinds[i], imp[3:6], scale)
         if kinds[i] == "limit":
             assert np.abs(imp[0:3]).max() < rel * scale, (i, imp[0:3], scale)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_kernel_resting_on_the_plane_carries_the_weight(precision):
+    """Static equilibrium on the kernel: the four lying poses of the oracle test, default physics (damping,
+    self-collision on), one substep per launch step (substeps = 1), zero actions for 1600 substeps (6.6 s); then over
+    4 substeps the ground's impulse H(q) (nu' - nu_free) is the weight's, M g 4 dt, within 2 %, horizontally under 6 %."""
+    states = D.lying_states()
+    n = len(states)
+    env = HumanoidVecEnv(n, seed=3, precision=precision, substeps=1, dt_env=DT)
+    env.reset()
+    env.set_state(phys=np.array(states))
+    zeros = torch.zeros(32, n, 17, device="cuda")
+    for _ in range(50):
+        env.step_k(zeros, autoreset=False)
+    seq = [env.get_state()[0]]
+    for _ in range(4):
+        env.step(np.zeros((n, 17), np.float32), autoreset=False)
+        seq.append(env.get_state()[0])
+    env.close()
+    w = D.MTOT * D.G * 4 * DT
+    for i in range(n):
+        J = D.ground_impulse_over(lambda: ((seq[j][i], seq[j + 1][i]) for j in range(4)))
+        assert abs(J[2] / w - 1) < 0.02, (i, J[2] / w)
+        assert np.hypot(J[0], J[1]) < 0.06 * J[2], (i, J)

@@ -24,7 +24,9 @@ reference's XML) and the oracle's forward kinematics (`om_link_frames`):
   impulses are equal and opposite (no net force); the ground only pushes (net impulse up) and its horizontal part
   stays inside the friction box's bound sqrt(2) mu times the vertical part;
 * over 0.1 s of free tumbling the energy and momentum drift halves with every halving of dt (first-order
-  consistency of the substep).
+  consistency of the substep);
+* static equilibrium: dropped onto the plane and left to settle, the ground's impulse over an env step is the
+  weight's.
 
 Bullet's link damping (0.04, default on) and MJCF joint damping are switched off where a conservation law is
 checked; contact, limit and damping semantics stay hypotheses about Bullet.  The GPU kernel
@@ -379,3 +381,51 @@ def test_integrator_drift_is_first_order(seed):
         assert d[-1] > 1e-9
         for a, b in zip(d, d[1:]):
             assert 1.8 < a / b < 2.2, d
+
+
+def lying_states():
+    """Four poses lying on the plane (on the back, front and both sides), 5 cm above it, at rest."""
+    out = []
+    for k, (ax, ang) in enumerate((("y", 90), ("y", -90), ("x", 90), ("x", -90))):
+        st = random_state(np.random.default_rng(3 + k), moving=False, z=0.0)
+        st[3:7] = Rotation.from_euler(ax, ang, degrees=True).as_quat()
+        st[2] -= O.parts(st)[:32, 2].min() - 0.05
+        out.append(st)
+    return out
+
+
+def ground_impulse_over(states_fn, nsub=4):
+    """The constraint impulse's base force rows summed over `nsub` consecutive substeps from a state, each substep's
+    H(q) (nu' - nu_free) with the env's default physics (damping on).  states_fn(s) -> the next substep's state."""
+    P1 = O.default_params()
+    P1.nsub = 1
+    tot = np.zeros(3)
+    s = None
+    for s, out in states_fn():
+        nu_free = nu_of(s) + P1.dt * O.aba(s, np.zeros(17), P1)
+        tot += (O.mass_matrix(s) @ (nu_of(out) - nu_free))[3:6]
+    return tot
+
+
+@pytest.mark.parametrize("pose", range(4))
+def test_resting_on_the_plane_the_ground_carries_the_weight(pose):
+    """Static equilibrium: dropped 5 cm onto the plane and left for 400 env steps (6.6 s, default physics, zero
+    torques), the ground's impulse over one env step's 4 substeps is the weight's, M g 4 dt, within 2 %, with a
+    horizontal part under 6 % of it."""
+    st = lying_states()[pose]
+    P = O.default_params()
+    for _ in range(400):
+        st = O.phys_step(st, np.zeros(17), P)
+    P1 = O.default_params()
+    P1.nsub = 1
+
+    def steps():
+        s = st.copy()
+        for _ in range(4):
+            out = O.phys_step(s, np.zeros(17), P1)
+            yield s, out
+            s = out
+    J = ground_impulse_over(steps)
+    w = MTOT * G * 4 * P1.dt
+    assert abs(J[2] / w - 1) < 0.02, J[2] / w
+    assert np.hypot(J[0], J[1]) < 0.06 * J[2]
