@@ -138,7 +138,8 @@ def test_kernel_limit_and_self_contact_impulses_are_internal(precision):
 def test_kernel_resting_on_the_plane_carries_the_weight(precision):
     """Static equilibrium on the kernel: the four lying poses of the oracle test, default physics (damping,
     self-collision on), one substep per launch step (substeps = 1), zero actions for 1600 substeps (6.6 s); then over
-    4 substeps the ground's impulse H(q) (nu' - nu_free) is the weight's, M g 4 dt, within 2 %, horizontally under 6 %."""
+    32 substeps the ground's impulse H(q) (nu' - nu_free) is the weight's, M g 32 dt, within 1 %, horizontally under
+    2 % (the settled body still rocks from substep to substep: fp32 lane 2 measured 0.973 over 4 substeps)."""
     states = D.lying_states()
     n = len(states)
     env = HumanoidVecEnv(n, seed=3, precision=precision, substeps=1, dt_env=DT)
@@ -148,12 +149,12 @@ def test_kernel_resting_on_the_plane_carries_the_weight(precision):
     for _ in range(50):
         env.step_k(zeros, autoreset=False)
     seq = [env.get_state()[0]]
-    for _ in range(4):
+    for _ in range(32):
         env.step(np.zeros((n, 17), np.float32), autoreset=False)
         seq.append(env.get_state()[0])
     env.close()
-    w = D.MTOT * D.G * 4 * DT
+    w = D.MTOT * D.G * 32 * DT
     for i in range(n):
-        J = D.ground_impulse_over(lambda: ((seq[j][i], seq[j + 1][i]) for j in range(4)))
-        assert abs(J[2] / w - 1) < 0.02, (i, J[2] / w)
-        assert np.hypot(J[0], J[1]) < 0.06 * J[2], (i, J)
+        J = D.ground_impulse_over(lambda: ((seq[j][i], seq[j + 1][i]) for j in range(32)))
+        assert abs(J[2] / w - 1) < 0.01, (i, J[2] / w)
+        assert np.hypot(J[0], J[1]) < 0.02 * J[2], (i, J)

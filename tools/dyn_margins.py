@@ -41,3 +41,27 @@ for prec in ("fp64", "fp32"):
         worst[2] = max(worst[2], np.abs(Ld).max() / (10 * rel * (np.abs(H[0:3] @ acc).max()
                                                                  + np.abs(np.cross(s0[i, 0:3], H[3:6] @ acc)).max())))
     print(prec, "free motion: worst / bound (power, P, L):", ["%.3g" % w for w in worst])
+
+# the resting equilibrium (tests/test_gpu_dynamics.py::test_kernel_resting_on_the_plane_carries_the_weight)
+import torch  # noqa: E402
+
+for prec in ("fp64", "fp32"):
+    states = D.lying_states()
+    n = len(states)
+    env = HumanoidVecEnv(n, seed=3, precision=prec, substeps=1, dt_env=DT)
+    env.reset()
+    env.set_state(phys=np.array(states))
+    zeros = torch.zeros(32, n, 17, device="cuda")
+    for _ in range(50):
+        env.step_k(zeros, autoreset=False)
+    seq = [env.get_state()[0]]
+    for _ in range(32):
+        env.step(np.zeros((n, 17), np.float32), autoreset=False)
+        seq.append(env.get_state()[0])
+    env.close()
+    w = D.MTOT * D.G * 32 * DT
+    out = []
+    for i in range(n):
+        J = D.ground_impulse_over(lambda: ((seq[j][i], seq[j + 1][i]) for j in range(32)))
+        out.append("%.4f/%.4f" % (J[2] / w, np.hypot(J[0], J[1]) / J[2]))
+    print(prec, "resting: vertical / weight, horizontal / vertical per pose:", out)
