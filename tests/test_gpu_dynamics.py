@@ -12,7 +12,8 @@ with Bullet's link damping, the MJCF joint damping and self-collision switched o
   model (oracle.mass_matrix: the Jacobian-summed H, independent of the kernel's articulated-body recursion);
 * constraint impulses, one substep (self-collision on where limbs overlap, joints past their limits elsewhere): no
   net force from self-contacts and limit rows, no net torque from limit rows;
-* static equilibrium (default physics): lying on the plane after 6.6 s, the ground carries the weight.
+* static equilibrium (default physics): lying on the plane, and on a 15 degree heightfield slope (friction
+  holding it), after 6.6 s the ground carries the weight.
 """
 import numpy as np
 import pytest
@@ -158,3 +159,32 @@ def test_kernel_resting_on_the_plane_carries_the_weight(precision):
         J = D.ground_impulse_over(lambda: ((seq[j][i], seq[j + 1][i]) for j in range(32)))
         assert abs(J[2] / w - 1) < 0.01, (i, J[2] / w)
         assert np.hypot(J[0], J[1]) < 0.02 * J[2], (i, J)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_kernel_resting_on_a_slope_friction_holds_the_weight(precision):
+    """The kernel on the oracle test's 15 degree heightfield slope (hum_set_terrain_ex, same heights): after 1600
+    single substeps the ground's impulse over 32 substeps is vertical and equal to the weight's within 1 %, although
+    every ground normal leans downhill - friction carries the tangential part."""
+    from ilrl_amd import _native as N
+    ter = D.slope_terrain()
+    states = D.lying_on_slope(ter)
+    n = len(states)
+    env = HumanoidVecEnv(n, seed=3, precision=precision, substeps=1, dt_env=DT)
+    env.set_terrain(N.HUM_TERRAIN_HEIGHTFIELD, heights=ter.heights, w=ter.w, l=ter.l, origin=ter.origin,
+                    centre=ter.mid)
+    env.reset()
+    env.set_state(phys=np.array(states))
+    zeros = torch.zeros(32, n, 17, device="cuda")
+    for _ in range(50):
+        env.step_k(zeros, autoreset=False)
+    seq = [env.get_state()[0]]
+    for _ in range(32):
+        env.step(np.zeros((n, 17), np.float32), autoreset=False)
+        seq.append(env.get_state()[0])
+    env.close()
+    w = D.MTOT * D.G * 32 * DT
+    for i in range(n):
+        J = D.ground_impulse_over(lambda: ((seq[j][i], seq[j + 1][i]) for j in range(32)))
+        assert abs(J[2] / w - 1) < 0.01, (i, J[2] / w)
+        assert np.hypot(J[0], J[1]) < 0.01 * J[2], (i, J)

@@ -25,8 +25,8 @@ reference's XML) and the oracle's forward kinematics (`om_link_frames`):
   stays inside the friction box's bound sqrt(2) mu times the vertical part;
 * over 0.1 s of free tumbling the energy and momentum drift halves with every halving of dt (first-order
   consistency of the substep);
-* static equilibrium: dropped onto the plane and left to settle, the ground's impulse over 32 substeps is the
-  weight's.
+* static equilibrium: dropped onto the plane, or onto a 15 degree heightfield slope (friction holding it), and
+  left to settle, the ground's impulse over 32 substeps is vertical and the weight's.
 
 Bullet's link damping (0.04, default on) and MJCF joint damping are switched off where a conservation law is
 checked; contact, limit and damping semantics stay hypotheses about Bullet.  The GPU kernel
@@ -429,3 +429,49 @@ def test_resting_on_the_plane_the_ground_carries_the_weight(pose):
     w = MTOT * G * 32 * P1.dt
     assert abs(J[2] / w - 1) < 0.01, J[2] / w
     assert np.hypot(J[0], J[1]) < 0.02 * J[2]
+
+
+SLOPE = 0.27   # a 15 degree planar heightfield z = SLOPE x + 0.3 (below the box friction's tan = mu = 1.6)
+
+
+def slope_terrain(w=64, l=64):
+    i, j = np.meshgrid(np.arange(w), np.arange(l), indexing="xy")   # vertex (i, j) at heights[i + j w]
+    h = (SLOPE * (i - (w - 1) / 2) + 0.3).astype(np.float32).reshape(-1)
+    return O.Terrain(O.TERRAIN_HEIGHTFIELD, heights=h, w=w, l=l, origin=(0.0, 0.0, 0.0))
+
+
+def lying_on_slope(ter):
+    out = []
+    for st in lying_states():
+        st = st.copy()
+        st[2] += SLOPE * st[0] + 0.3 - ter.mid
+        out.append(st)
+    return out
+
+
+@pytest.mark.parametrize("pose", range(4))
+def test_resting_on_a_slope_friction_holds_the_weight(pose):
+    """Static equilibrium on a 15 degree heightfield slope: the contact normals lean downhill, so only friction can
+    make the ground's force cancel gravity - after 400 env steps the ground's impulse over 32 substeps is vertical
+    and equal to the weight's within 1 % (its horizontal part under 1 % of it)."""
+    ter = slope_terrain()
+    st = lying_on_slope(ter)[pose]
+    P = ter.apply(O.default_params())
+    for _ in range(400):
+        st = O.phys_step(st, np.zeros(17), P)
+    P1 = ter.apply(O.default_params())
+    P1.nsub = 1
+    con = O.contacts(st, P1)
+    nz = con[con[:, 1] < 0][:, 7:10]
+    np.testing.assert_allclose(nz, np.tile([-SLOPE, 0, 1] / np.hypot(SLOPE, 1), (len(nz), 1)), atol=1e-6)
+
+    def steps():
+        s = st.copy()
+        for _ in range(32):
+            out = O.phys_step(s, np.zeros(17), P1)
+            yield s, out
+            s = out
+    J = ground_impulse_over(steps)
+    w = MTOT * G * 32 * P1.dt
+    assert abs(J[2] / w - 1) < 0.01, J[2] / w
+    assert np.hypot(J[0], J[1]) < 0.01 * J[2], J
