@@ -59,9 +59,10 @@ def parse():
                          "gather) even with one rank: the RCCL code path on a one-GPU box, where RCCL refuses two ranks "
                          "on one device")
     ap.add_argument("--transport", default="dma", choices=["dma", "collective"],
-                    help="the trajectory gather's transport for N > 1: dma = rank 0 pulls every rank's packed fragment "
-                         "with the SDMA copy engines over IPC-mapped buffers (parallel.DmaGather: no compute unit, so "
-                         "it overlaps the env launches); collective = one dist.gather per fragment (RCCL kernels, which "
+                    help="the trajectory gather's transport for N > 1: dma = rank 0 pulls every launch's rows of "
+                         "every rank's packed fragment with the SDMA copy engines over IPC-mapped buffers "
+                         "(parallel.DmaGather: no compute unit, so it overlaps the next launch; the run ends on a short "
+                         "drain launch, launch_plan); collective = one dist.gather per fragment (RCCL kernels, which "
                          "wait for the env launch to leave the CUs)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: host-staged, tests)")
