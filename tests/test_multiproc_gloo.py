@@ -103,9 +103,10 @@ def _tg_worker(rank, world, port, n_total, q):
     for s, kk in enumerate(sizes):
         slot = (t // G) % 2
         tg.pack(slot, t % G, rows(t, kk))
+        final = (t + kk) % G == 0 or s == len(sizes) - 1
+        tg.commit(slot, t % G, t % G + kk, final)   # bench.py's per-launch call: the fragment goes on the final one
         t += kk
-        if t % G == 0 or s == len(sizes) - 1:
-            tg.start(slot)
+        if final:
             tg.wait(slot)
             r = tg.result(slot)
             if r is not None:
